@@ -1,0 +1,207 @@
+"""NRMS scoring throughput on MI355X (BASELINE.json metric / config 3).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch 1024] [--proj folded|direct|auto]
+
+One step = one full NRMS forward (src/model/NRMS/__init__.py:19-48, eval
+mode) over a batch of B synthetic MIND-shaped impressions resident in HBM:
+1+K = 5 candidate titles and 50 clicked titles of 20 tokens each (history
+left-padded with all-zero titles, src/dataset.py:79-83), V = 70,976 words,
+d = 300, 15 heads, query dim 200 — every title is encoded (forward semantics).
+For N > 1 (torch.distributed.run, one process per GPU) each rank scores its
+own user shard of B impressions (weak scaling, no data-path collective); the
+time is the max over ranks. Rank 0 prints one JSON line.
+
+Extra fields: per-stage milliseconds (HIP events on the launch stream), the
+roofline of the dominant kernel, and the CPU baseline (oracle ATen-order
+restatement timed on this host, kind "port") with a parity check of the GPU
+logits against it on the same sample.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "impressions/sec scored (NRMS, MIND-shape) at 1/2/4/8 MI355X; AUC vs CPU ref"
+V_WORDS, D, L, C, N_CLICKED = 70976, 300, 20, 5, 50
+PEAK_TFLOPS_F32 = 157.3   # MI355X fp32 MFMA/VALU dense peak (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0     # HBM3E spec peak
+
+
+def synth_titles(gen, n, V, device):
+    ids = torch.randint(1, V, (n, L), generator=gen, device=device)
+    lens = torch.randint(5, L + 1, (n, 1), generator=gen, device=device)
+    return torch.where(torch.arange(L, device=device)[None] < lens, ids, torch.zeros_like(ids))
+
+
+def synth_impressions(seed, B, V, device):
+    """SURVEY §8d synthetic inputs: candidates [B,C,L], clicked [B,N,L]."""
+    gen = torch.Generator(device=device).manual_seed(seed)
+    cand = synth_titles(gen, B * C, V, device).view(B, C, L)
+    clk = synth_titles(gen, B * N_CLICKED, V, device).view(B, N_CLICKED, L)
+    hist = torch.randint(1, N_CLICKED + 1, (B, 1), generator=gen, device=device)
+    pad = torch.arange(N_CLICKED, device=device)[None] < (N_CLICKED - hist)
+    clk = torch.where(pad[:, :, None], torch.zeros_like(clk), clk)
+    return cand.contiguous(), clk.contiguous()
+
+
+def build_model(device, seed=0):
+    from newsrecommendationsystem_amd import NRMS, NRMSConfig
+
+    class Cfg(NRMSConfig):
+        hip_check_ids = False   # inputs are generated in range on the device
+
+    torch.manual_seed(seed)
+    emb = torch.randn(V_WORDS, D)  # N(0,1), row 0 not zeroed (data_preprocess.py:272-277)
+    return NRMS(Cfg, emb).to(device).eval()
+
+
+def load_traffic(kernel):
+    """Per-launch HBM bytes of `kernel` from the committed PMC summary (rocprofv3
+    --pmc FETCH_SIZE / WRITE_SIZE, gfx950-corrected), or None."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(model, device, sample_B=32, min_seconds=10.0, max_reps=5):
+    """Time the oracle's ATen-order CPU restatement (oracle/nrms_torch_cpu.py)
+    on a bounded sample of the same workload; also check GPU parity on it."""
+    from oracle import nrms_torch_cpu as T
+    cand, clk = synth_impressions(424242, sample_B, V_WORDS, device)
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    cand_c, clk_c = cand.cpu(), clk.cpu()
+    threads = torch.get_num_threads()
+    with torch.no_grad():
+        ref = T.forward(cand_c, clk_c, sd)  # warm
+        reps, t0 = 0, time.perf_counter()
+        while reps < max_reps and (reps == 0 or time.perf_counter() - t0 < min_seconds):
+            ref = T.forward(cand_c, clk_c, sd)
+            reps += 1
+        dt = time.perf_counter() - t0
+        gpu = model.forward_ids(cand, clk).cpu()
+    err = float(((gpu - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-30)).max())
+    value = sample_B * reps / dt
+    info = {"value": round(value, 2), "unit": "impressions/s", "cores": threads, "kind": "port",
+            "sample": f"{reps} x NRMS.forward over {sample_B} impressions (1+K=5, 50 clicked, L=20, "
+                      f"V={V_WORDS}) via oracle/nrms_torch_cpu.py, torch {torch.__version__}, "
+                      f"{threads} threads, {dt:.1f} s"}
+    parity = {"sample_impressions": sample_B, "max_normwise_rel_err_logits": err,
+              "tolerance": 1e-3, "ok": bool(err <= 1e-3)}
+    return info, parity
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1024, help="impressions per GPU per step")
+    ap.add_argument("--proj", choices=["folded", "direct", "auto"], default="folded")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+    device = torch.device("cuda", local)
+    torch.cuda.set_device(device)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    from newsrecommendationsystem_amd import _native as Nat
+    from newsrecommendationsystem_amd.pipeline import ForwardPlan
+
+    mode = {"folded": Nat.NRMS_PROJ_FOLDED, "direct": Nat.NRMS_PROJ_DIRECT, "auto": Nat.NRMS_PROJ_AUTO}[args.proj]
+    model = build_model(device)
+    B = args.batch
+    cand, clk = synth_impressions(1000 + rank, B, V_WORDS, device)   # this rank's user shard
+    plan = ForwardPlan(model, B, C, N_CLICKED, L, proj_mode=mode)
+    n_st = len(plan.stages)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            plan.run(cand, clk)
+        # one un-timed check that the plan equals the fused C-ABI forward
+        y_plan = plan.run(cand, clk).clone()
+        y_fwd = model.forward_ids(cand, clk, proj_mode=mode)
+        same = bool(torch.equal(y_plan, y_fwd))
+        events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_st + 1)]
+                  for _ in range(args.steps)]
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            plan.run(cand, clk, events[k])
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    stage_ms = {s: 0.0 for s in plan.stages}
+    for ev in events:
+        for i, s in enumerate(plan.stages):
+            stage_ms[s] += ev[i].elapsed_time(ev[i + 1])
+    stage_ms = {s: v / args.steps for s, v in stage_ms.items()}
+    work = plan.work()
+    dom = max(stage_ms, key=stage_ms.get)
+    w = work[dom]
+    t_dom = stage_ms[dom] / 1e3
+    intensity = w["flop"] / max(w["bytes"], 1)
+    if intensity >= PEAK_TFLOPS_F32 * 1e12 / (PEAK_HBM_GBS * 1e9):
+        achieved, peak, unit, bound = w["flop"] / t_dom / 1e12, PEAK_TFLOPS_F32, "TFLOP/s", "mfma"
+    else:
+        achieved, peak, unit, bound = w["bytes"] / t_dom / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = world * B * args.steps / elapsed
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "impressions/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "data": "synthetic (MIND-shaped ids, random-init weights, N(0,1) embedding table)",
+        "config": {"workload": "BASELINE cfg3: full NRMS forward scoring (news+user encoder+"
+                               "click predictor), every title encoded", "global_batch": B * world,
+                   "impressions_per_gpu": B, "candidates": C, "clicked": N_CLICKED,
+                   "title_len": L, "vocab": V_WORDS, "d_model": D, "heads": 15,
+                   "query_dim": 200, "proj_mode": args.proj, "parallelism": f"user-shard x{world}"},
+        "roofline": {"kernel": dom, "bound": bound, "achieved": round(achieved, 3),
+                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
+                     "traffic": load_traffic(dom),
+                     "algorithmic_per_launch": {"flop": w["flop"], "bytes": w["bytes"]}},
+        "stages_ms": {s: round(v, 4) for s, v in stage_ms.items()},
+        "plan_equals_nrms_forward": same,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cb, parity = cpu_baseline(model, device)
+        out["cpu_baseline"] = cb
+        out["parity_vs_cpu"] = parity
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,159 @@
+/*
+ * nrms_hip.h — C ABI of the MI355X (gfx950) NRMS scoring library
+ * (libnrms_hip.so, built from newsrecommendationsystem_amd/csrc/).
+ *
+ * Drop-in boundary for the NRMS scoring path of Maguire1999/
+ * NewsRecommendationSystem (paths below are relative to that repo). The
+ * reference is PyTorch only and has no FFI of its own; each entry point here
+ * replaces the ATen op sequence of one reference method, cited per function.
+ * The Python host mirror (newsrecommendationsystem_amd/nrms.py) binds these
+ * through ctypes behind the reference's own NRMS module interface.
+ *
+ * Conventions
+ *   - All tensor arguments are caller-allocated DEVICE pointers, borrowed for
+ *     the call. The library never allocates or frees, never synchronises the
+ *     stream, and keeps no state: any host thread may call it on any stream,
+ *     and every call is capturable into a hipGraph.
+ *   - fp32 row-major everywhere; ids are int64 (the reference's LongTensor).
+ *   - Every function returns NRMS_OK (0) or an nrms_status_t error code; a
+ *     launch failure returns NRMS_ERR_HIP and the HIP error is kept for
+ *     nrms_last_hip_error().
+ *   - Kernels assume ids are in [0, V); callers validate (the Python glue does,
+ *     mirroring nn.Embedding's IndexError). An out-of-range id never reads out
+ *     of bounds: its row is produced as NaN.
+ *   - Eval-mode semantics (dropout = identity, src/model/NRMS/news_encoder.py:
+ *     38-40,43-45). Training kernels are not part of this ABI version.
+ */
+#ifndef NRMS_HIP_H
+#define NRMS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NRMS_ABI_VERSION 1
+
+typedef enum {
+  NRMS_OK = 0,
+  NRMS_ERR_INVALID_ARG = 1,   /* null pointer, negative size, misalignment   */
+  NRMS_ERR_UNSUPPORTED = 2,   /* shape outside the compiled kernel set       */
+  NRMS_ERR_WORKSPACE = 3,     /* workspace missing or too small              */
+  NRMS_ERR_HIP = 4            /* a HIP launch/API call failed                */
+} nrms_status_t;
+
+/* One encoder's parameters (device pointers), nn.Linear layout [out, in].
+ * Mirrors MultiHeadSelfAttention (src/model/general/attention/
+ * multihead_self.py:27-44) + AdditiveAttention (src/model/general/attention/
+ * additive.py:13-20). */
+typedef struct {
+  const float* w_q; const float* b_q;   /* [D, D], [D] */
+  const float* w_k; const float* b_k;   /* [D, D], [D] */
+  const float* w_v; const float* b_v;   /* [D, D], [D] */
+  const float* w_add; const float* b_add; /* additive linear [Q, D], [Q] */
+  const float* q_add;                   /* attention_query_vector [Q]  */
+  int32_t d_model;                      /* D  (300)                    */
+  int32_t n_heads;                      /* H  (15); D / H must be 20   */
+  int32_t query_dim;                    /* Q  (200); must be <= 208    */
+} nrms_encoder_weights_t;
+
+/* News-encoder projection strategy. FOLDED projects the whole vocabulary once
+ * (qkv_table[V, 3D] = E W^T + b) and gathers projected rows per token; DIRECT
+ * gathers embedding rows and projects every token. Both give the same result
+ * (each projected row depends only on its token id); AUTO picks FOLDED when
+ * the batch has more tokens than the vocabulary. */
+typedef enum { NRMS_PROJ_AUTO = 0, NRMS_PROJ_DIRECT = 1, NRMS_PROJ_FOLDED = 2 } nrms_proj_mode_t;
+
+int32_t nrms_abi_version(void);
+const char* nrms_status_string(int32_t status);
+int32_t nrms_last_hip_error(void);
+
+/* nn.Embedding forward (src/model/NRMS/news_encoder.py:38): out[t,:] =
+ * table[ids[t],:] for t < n_tok, bit-exact copy; id 0 is gathered like any id. */
+int32_t nrms_embedding_gather(const int64_t* ids, int64_t n_tok, const float* table,
+                              int64_t V, int32_t D, float* out, hipStream_t stream);
+
+/* Q|K|V projection (multihead_self.py:53-58): qkv[m, 0:3D] = x[row(m)] [W_Q;W_K;W_V]^T
+ * + [b_Q;b_K;b_V], row(m) = row_ids ? row_ids[m] : m (row_ids index x's rows,
+ * n_rows_x bounds them). fp32 MFMA GEMM. */
+int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
+                         const nrms_encoder_weights_t* w, float* qkv, hipStream_t stream);
+
+/* Multi-head raw-exp self-attention over sequences of length L
+ * (ScaledDotProductAttention, multihead_self.py:15-23, heads concatenated
+ * :74-75): for sequence s, token i reads qkv row r(s,i) = tok_ids ?
+ * tok_ids[s*L+i] : s*L+i (tok_ids index qkv's n_rows_qkv rows). Sequences
+ * s >= n_seq_a take their ids from tok_ids_b + (s-n_seq_a)*L (NULL: same
+ * array). ctx[s*L+i, :] is the [D] context row. L <= 64. */
+int32_t nrms_self_attention(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
+                            int64_t n_seq_a, const int64_t* tok_ids_b, int64_t n_seq,
+                            int32_t L, const nrms_encoder_weights_t* w, float* ctx,
+                            hipStream_t stream);
+
+/* AdditiveAttention (additive.py:27-53) over x[n_seq, L, D]:
+ * out[s] = sum_l softmax_l(tanh(x W^T + b) . q) x[s,l]. scores_ws: device
+ * scratch of n_seq*L floats. */
+int32_t nrms_additive_attention(const float* x, int64_t n_seq, int32_t L,
+                                const nrms_encoder_weights_t* w, float* scores_ws,
+                                float* out, hipStream_t stream);
+
+/* The two halves of nrms_additive_attention, for callers that time or fuse
+ * them separately: per-token scores[m] = tanh(x[m] W^T + b) . q for m <
+ * n_rows (additive.py:35-38; the [n_rows, Q] tile stays in registers), and
+ * the pooling out[s] = sum_l softmax_l(scores[s, :]) x[s, l] (:39,51-52). */
+int32_t nrms_additive_scores(const float* x, int64_t n_rows, const nrms_encoder_weights_t* w,
+                             float* scores, hipStream_t stream);
+int32_t nrms_additive_pool(const float* x, const float* scores, int64_t n_seq, int32_t L,
+                           int32_t D, float* out, hipStream_t stream);
+
+/* NewsEncoder.forward (src/model/NRMS/news_encoder.py:27-48), eval mode:
+ * ids[n_titles, L] -> out[n_titles, D]. */
+size_t nrms_news_encode_workspace_size(int64_t n_titles, int32_t L, int64_t V, int32_t D,
+                                       int32_t proj_mode);
+int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const float* table,
+                         int64_t V, const nrms_encoder_weights_t* w, int32_t proj_mode,
+                         float* out, void* workspace, size_t workspace_bytes,
+                         hipStream_t stream);
+
+/* Same, from a caller-held folded table qkv_table[V, 3D] (nrms_qkv_project of
+ * the whole embedding table): lets an eval loop reuse one projection across
+ * calls while the weights are unchanged. */
+size_t nrms_news_encode_folded_workspace_size(int64_t n_titles, int32_t L, int32_t D);
+int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
+                                const float* qkv_table, int64_t V,
+                                const nrms_encoder_weights_t* w, float* out,
+                                void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* UserEncoder.forward (src/model/NRMS/user_encoder.py:15-26): clicked[B, N, D]
+ * (row-major, contiguous) -> out[B, D]. */
+size_t nrms_user_encode_workspace_size(int64_t B, int32_t N, int32_t D);
+int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N,
+                         const nrms_encoder_weights_t* w, float* out, void* workspace,
+                         size_t workspace_bytes, hipStream_t stream);
+
+/* DotProductClickPredictor.forward (src/model/general/click_predictor/
+ * dot_product.py:8-19): out[b, c] = <news[b*stride_b + c*stride_c, :], user[b*stride_u, :]>,
+ * strides in floats. Also NRMS.get_prediction (src/model/NRMS/__init__.py:73-84)
+ * with B = 1. */
+int32_t nrms_score(const float* news, int64_t B, int32_t C, int64_t stride_b,
+                   int64_t stride_c, const float* user, int64_t stride_u, int32_t D,
+                   float* out, hipStream_t stream);
+
+/* NRMS.forward (src/model/NRMS/__init__.py:19-48), eval mode:
+ * cand_ids[B, C, L], clicked_ids[B, N, L] -> logits[B, C]. All B*(C+N) titles
+ * are encoded (forward semantics), then the user vector and the scores. */
+size_t nrms_forward_workspace_size(int64_t B, int32_t C, int32_t N, int32_t L, int64_t V,
+                                   int32_t D, int32_t proj_mode);
+int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_t B, int32_t C,
+                     int32_t N, int32_t L, const float* table, int64_t V,
+                     const nrms_encoder_weights_t* news_w, const nrms_encoder_weights_t* user_w,
+                     int32_t proj_mode, float* logits, void* workspace, size_t workspace_bytes,
+                     hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NRMS_HIP_H */

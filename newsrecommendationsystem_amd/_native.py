@@ -1,0 +1,104 @@
+"""ctypes binding of libnrms_hip.so (C ABI: include/nrms_hip.h).
+
+The library is the product path: if it is missing or fails to load, every
+entry point raises — there is no eager / CPU fallback. Torch is imported first
+so the library binds to the HIP runtime torch already loaded (same soname),
+letting torch's stream handles and device pointers be passed straight in.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
+
+_PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_PKG, "libnrms_hip.so")
+ABI_VERSION = 1
+
+NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
+
+_p = ctypes.c_void_p
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_sz = ctypes.c_size_t
+
+
+class EncoderWeights(ctypes.Structure):
+    """nrms_encoder_weights_t."""
+    _fields_ = [("w_q", _p), ("b_q", _p), ("w_k", _p), ("b_k", _p), ("w_v", _p), ("b_v", _p),
+                ("w_add", _p), ("b_add", _p), ("q_add", _p),
+                ("d_model", _i32), ("n_heads", _i32), ("query_dim", _i32)]
+
+
+_EW = ctypes.POINTER(EncoderWeights)
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "nrms_abi_version": (_i32, []),
+    "nrms_status_string": (ctypes.c_char_p, [_i32]),
+    "nrms_last_hip_error": (_i32, []),
+    "nrms_embedding_gather": (_i32, [_p, _i64, _p, _i64, _i32, _p, _p]),
+    "nrms_qkv_project": (_i32, [_p, _i64, _p, _i64, _EW, _p, _p]),
+    "nrms_self_attention": (_i32, [_p, _i64, _p, _i64, _p, _i64, _i32, _EW, _p, _p]),
+    "nrms_additive_attention": (_i32, [_p, _i64, _i32, _EW, _p, _p, _p]),
+    "nrms_additive_scores": (_i32, [_p, _i64, _EW, _p, _p]),
+    "nrms_additive_pool": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),
+    "nrms_news_encode_workspace_size": (_sz, [_i64, _i32, _i64, _i32, _i32]),
+    "nrms_news_encode": (_i32, [_p, _i64, _i32, _p, _i64, _EW, _i32, _p, _p, _sz, _p]),
+    "nrms_news_encode_folded_workspace_size": (_sz, [_i64, _i32, _i32]),
+    "nrms_news_encode_folded": (_i32, [_p, _i64, _i32, _p, _i64, _EW, _p, _p, _sz, _p]),
+    "nrms_user_encode_workspace_size": (_sz, [_i64, _i32, _i32]),
+    "nrms_user_encode": (_i32, [_p, _i64, _i32, _EW, _p, _p, _sz, _p]),
+    "nrms_score": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p]),
+    "nrms_forward_workspace_size": (_sz, [_i64, _i32, _i32, _i32, _i64, _i32, _i32]),
+    "nrms_forward": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _p, _i64, _EW, _EW, _i32, _p, _p,
+                            _sz, _p]),
+}
+
+_lib = None
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+def load():
+    """Load and type the library once; raise loudly if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise NativeError(
+            f"{LIB_PATH} not found: build it with `python -m newsrecommendationsystem_amd.build` "
+            "(there is no CPU or eager fallback for the NRMS HIP path)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    v = lib.nrms_abi_version()
+    if v != ABI_VERSION:
+        raise NativeError(f"libnrms_hip ABI {v} != expected {ABI_VERSION}")
+    _lib = lib
+    return lib
+
+
+def check(status, what):
+    if status != 0:
+        lib = load()
+        msg = lib.nrms_status_string(status).decode()
+        hip = lib.nrms_last_hip_error()
+        raise NativeError(f"{what} failed: {msg} (status {status}, hip error {hip})")
+
+
+def call(name, *args):
+    fn = getattr(load(), name)
+    check(fn(*args), name)
+
+
+def ptr(t):
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def stream_handle(device=None):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,79 @@
+"""Build libnrms_hip.so in-tree for gfx950 (hipcc cross-compiles without a GPU).
+
+    python -m newsrecommendationsystem_amd.build [--force]
+
+The .so lands next to this file so it travels to the GPU box with the repo
+snapshot (it is git-ignored, not gpurun-ignored).
+"""
+import argparse
+import concurrent.futures as cf
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+OBJ = os.path.join(PKG, "_build")
+LIB = os.path.join(PKG, "libnrms_hip.so")
+SOURCES = ["gather.hip", "gemm_f32.hip", "attention.hip", "score.hip", "capi.hip"]
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = "gfx950"
+FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
+         "-Wall", "-Wno-unused-function"]
+
+
+def _newer(src_paths, dst):
+    if not os.path.exists(dst):
+        return True
+    t = os.path.getmtime(dst)
+    return any(os.path.getmtime(p) > t for p in src_paths)
+
+
+def _deps():
+    return [os.path.join(CSRC, "nrms_common.hpp"), os.path.join(INCLUDE, "nrms_hip.h")]
+
+
+def build(force=False, verbose=True):
+    os.makedirs(OBJ, exist_ok=True)
+    jobs = []
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(OBJ, s.replace(".hip", ".o"))
+        if force or _newer([src] + _deps(), obj):
+            jobs.append((src, obj))
+
+    def compile_one(job):
+        src, obj = job
+        cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+        return src, r.stderr
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, max(1, len(jobs)))) as ex:
+        for src, err in ex.map(compile_one, jobs):
+            if verbose:
+                print(f"[nrms build] compiled {os.path.basename(src)}")
+                if err.strip():
+                    print(err)
+    objs = [os.path.join(OBJ, s.replace(".hip", ".o")) for s in SOURCES]
+    if force or jobs or _newer(objs, LIB):
+        tmp = LIB + ".tmp"
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp] + objs
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, LIB)
+        if verbose:
+            print(f"[nrms build] linked {LIB}")
+    return LIB
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    build(force=a.force)
+    sys.exit(0)

@@ -1,0 +1,199 @@
+// Multi-head raw-exp self-attention and additive-attention pooling.
+//
+// mhsa_rawexp_kernel restates ScaledDotProductAttention
+// (src/model/general/attention/multihead_self.py:15-23) exactly as the
+// reference normalises: e = exp(QK^T / sqrt(d_k)) with NO max subtraction,
+// attn = e / (sum(e) + 1e-8), ctx = attn · V, heads concatenated in head
+// order (:74-75). Overflow therefore yields inf/inf = NaN and all-underflow
+// yields a zero context, as in the reference.
+//
+// One workgroup per sequence (a title, L = 20, or a user history, L = 50).
+// K|V of the whole sequence (L x 2D floats) are staged once in LDS; each lane
+// owns one (query token, head) task: its q slice lives in registers, the L raw
+// exps stay in registers between the two passes, and K/V rows are read with
+// ds_read_b128 (lanes of one head read the same address: broadcast).
+//
+// additive_pool_kernel restates the second half of AdditiveAttention
+// (src/model/general/attention/additive.py:37-52): a standard max-subtracted
+// softmax over the per-token scores (produced by the fused GEMM epilogue) and
+// the weighted sum of the token rows. One wave per sequence.
+#include "nrms_common.hpp"
+
+#include <mutex>
+
+namespace nrms {
+namespace {
+
+template <int LMAX, int DK, int H, int NT>
+__global__ __launch_bounds__(NT) void mhsa_rawexp_kernel(
+    const float* __restrict__ qkv, int64_t n_rows, const int64_t* __restrict__ ids_a,
+    int64_t n_seq_a, const int64_t* __restrict__ ids_b, int L, float* __restrict__ ctx) {
+  extern __shared__ __attribute__((aligned(16))) float kv[];  // [L][2D] then row ids
+  constexpr int D = H * DK;
+  constexpr int ld = 3 * D;
+  const int64_t s = blockIdx.x;
+  const int tid = threadIdx.x;
+
+  const int64_t* ids = nullptr;
+  if (ids_a) ids = (s < n_seq_a || ids_b == nullptr) ? ids_a + s * L : ids_b + (s - n_seq_a) * L;
+  int64_t* rowidx = reinterpret_cast<int64_t*>(kv + (size_t)L * 2 * D);
+  for (int i = tid; i < L; i += NT) {
+    const int64_t r = ids ? ids[i] : s * L + i;
+    rowidx[i] = ((uint64_t)r < (uint64_t)n_rows) ? r : -1;
+  }
+  __syncthreads();
+
+  constexpr int d2q = (2 * D) / 4;  // float4 per K|V row
+  for (int e = tid; e < L * d2q; e += NT) {
+    const int i = e / d2q;
+    const int c = e - i * d2q;
+    const int64_t r = rowidx[i];
+    const float4 v = r >= 0 ? *reinterpret_cast<const float4*>(qkv + r * ld + D + 4 * c) : nan4();
+    *reinterpret_cast<float4*>(kv + (size_t)i * 2 * D + 4 * c) = v;
+  }
+  __syncthreads();
+
+  // 1/sqrt(d_k) in fp32; the reference divides by np.sqrt(d_k) (1-ulp apart).
+  const float rs = 1.0f / sqrtf((float)DK);
+  for (int task = tid; task < L * H; task += NT) {
+    const int h = task / L;
+    const int i = task - h * L;
+    const int64_t r = rowidx[i];
+
+    float q[DK];
+    if (r >= 0) {
+      const float4* qp = reinterpret_cast<const float4*>(qkv + r * ld + h * DK);
+#pragma unroll
+      for (int t = 0; t < DK / 4; ++t) {
+        const float4 v = qp[t];
+        q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < DK; ++t) q[t] = qnan();
+    }
+
+    float e[LMAX];
+    float sum = 0.f;
+#pragma unroll
+    for (int j = 0; j < LMAX; ++j) {
+      if (j < L) {
+        const float4* kr = reinterpret_cast<const float4*>(kv + (size_t)j * 2 * D + h * DK);
+        float d = 0.f;
+#pragma unroll
+        for (int t = 0; t < DK / 4; ++t) {
+          const float4 k4 = kr[t];
+          d = fmaf(q[4 * t], k4.x, d);
+          d = fmaf(q[4 * t + 1], k4.y, d);
+          d = fmaf(q[4 * t + 2], k4.z, d);
+          d = fmaf(q[4 * t + 3], k4.w, d);
+        }
+        e[j] = expf(d * rs);
+        sum += e[j];
+      } else {
+        e[j] = 0.f;
+      }
+    }
+    const float inv = 1.0f / (sum + 1e-8f);
+
+    float acc[DK];
+#pragma unroll
+    for (int t = 0; t < DK; ++t) acc[t] = 0.f;
+#pragma unroll
+    for (int j = 0; j < LMAX; ++j) {
+      if (j < L) {
+        const float a = e[j] * inv;
+        const float4* vr = reinterpret_cast<const float4*>(kv + (size_t)j * 2 * D + D + h * DK);
+#pragma unroll
+        for (int t = 0; t < DK / 4; ++t) {
+          const float4 v4 = vr[t];
+          acc[4 * t] = fmaf(a, v4.x, acc[4 * t]);
+          acc[4 * t + 1] = fmaf(a, v4.y, acc[4 * t + 1]);
+          acc[4 * t + 2] = fmaf(a, v4.z, acc[4 * t + 2]);
+          acc[4 * t + 3] = fmaf(a, v4.w, acc[4 * t + 3]);
+        }
+      }
+    }
+    float4* op = reinterpret_cast<float4*>(ctx + (s * L + i) * D + h * DK);
+#pragma unroll
+    for (int t = 0; t < DK / 4; ++t)
+      op[t] = make_float4(acc[4 * t], acc[4 * t + 1], acc[4 * t + 2], acc[4 * t + 3]);
+  }
+}
+
+constexpr int kPoolThreads = 256;
+
+__global__ __launch_bounds__(kPoolThreads) void additive_pool_kernel(
+    const float* __restrict__ x, const float* __restrict__ score, int64_t n_seq, int L, int D,
+    float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t s = (int64_t)blockIdx.x * (kPoolThreads / kWave) + (threadIdx.x >> 6);
+  if (s >= n_seq) return;
+  const float v = lane < L ? score[s * L + lane] : -INFINITY;
+  const float m = wave_max_nan(v);
+  const float e = lane < L ? expf(v - m) : 0.f;
+  const float sum = wave_sum(e);
+  const float w = e / sum;
+  const int d4 = D / 4;
+  const float4* xs = reinterpret_cast<const float4*>(x + s * L * D);
+  float4* os = reinterpret_cast<float4*>(out + s * D);
+  for (int c = lane; c < d4; c += kWave) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int l = 0; l < L; ++l) {
+      const float wl = __shfl(w, l);
+      const float4 xv = xs[l * d4 + c];
+      acc.x = fmaf(wl, xv.x, acc.x);
+      acc.y = fmaf(wl, xv.y, acc.y);
+      acc.z = fmaf(wl, xv.z, acc.z);
+      acc.w = fmaf(wl, xv.w, acc.w);
+    }
+    os[c] = acc;
+  }
+}
+
+template <int LMAX, int NT>
+int32_t launch_mhsa_inst(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
+                         const int64_t* ids_b, int64_t n_seq, int L, float* ctx, hipStream_t s) {
+  constexpr int DK = 20, H = 15;
+  constexpr int D = H * DK;
+  const size_t lds = (size_t)L * 2 * D * sizeof(float) + (size_t)L * sizeof(int64_t);
+  if (lds > 160 * 1024) return NRMS_ERR_UNSUPPORTED;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mhsa_rawexp_kernel<LMAX, DK, H, NT>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  });
+  hipLaunchKernelGGL((mhsa_rawexp_kernel<LMAX, DK, H, NT>), dim3((unsigned)n_seq), dim3(NT), lds,
+                     s, qkv, n_rows, ids_a, n_seq_a, ids_b, L, ctx);
+  return launch_status();
+}
+
+}  // namespace
+
+int32_t launch_mhsa(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
+                    const int64_t* ids_b, int64_t n_seq, int L, int H, int DK, float* ctx,
+                    hipStream_t s) {
+  if (n_seq == 0) return NRMS_OK;
+  // Compiled for the reference configuration: d_k = 20, 15 heads (config.py:34,45).
+  if (DK != 20 || H != 15 || L < 1 || L > 64) return NRMS_ERR_UNSUPPORTED;
+  if (((uintptr_t)qkv % 16) != 0 || ((uintptr_t)ctx % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  if (n_seq > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  if (L <= 20) return launch_mhsa_inst<20, 320>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
+  if (L <= 32) return launch_mhsa_inst<32, 512>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
+  if (L <= 50) return launch_mhsa_inst<50, 768>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
+  return launch_mhsa_inst<64, 1024>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
+}
+
+int32_t launch_additive_pool(const float* x, const float* score, int64_t n_seq, int L, int D,
+                             float* out, hipStream_t s) {
+  if (n_seq == 0) return NRMS_OK;
+  if (L < 1 || L > 64 || D % 4 != 0) return NRMS_ERR_UNSUPPORTED;
+  if (((uintptr_t)x % 16) != 0 || ((uintptr_t)out % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  const int per = kPoolThreads / kWave;
+  const int64_t blocks = (n_seq + per - 1) / per;
+  hipLaunchKernelGGL(additive_pool_kernel, dim3((unsigned)blocks), dim3(kPoolThreads), 0, s, x,
+                     score, n_seq, L, D, out);
+  return launch_status();
+}
+
+}  // namespace nrms

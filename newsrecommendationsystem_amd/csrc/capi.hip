@@ -1,0 +1,315 @@
+// C ABI (include/nrms_hip.h): argument validation, workspace carving and the
+// stage order of the NRMS encoders. Stateless; every call only enqueues work
+// on the caller's stream (no allocation, no synchronisation).
+#include "nrms_common.hpp"
+
+namespace nrms {
+
+static thread_local int32_t g_last_hip = 0;
+void set_last_hip_error(hipError_t e) { g_last_hip = (int32_t)e; }
+
+namespace {
+
+constexpr int kDK = 20;   // d_k = D / H supported by the attention kernel
+constexpr int kQMax = 208;
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Bump allocator over the caller's workspace.
+struct Carve {
+  char* base;
+  size_t cap, off = 0;
+  bool ok = true;
+  float* floats(size_t n) {
+    const size_t need = align_up(n * sizeof(float));
+    if (off + need > cap) { ok = false; return nullptr; }
+    float* p = reinterpret_cast<float*>(base + off);
+    off += need;
+    return p;
+  }
+};
+
+bool weights_ok(const nrms_encoder_weights_t* w) {
+  if (!w) return false;
+  if (!w->w_q || !w->b_q || !w->w_k || !w->b_k || !w->w_v || !w->b_v || !w->w_add ||
+      !w->b_add || !w->q_add)
+    return false;
+  return w->d_model > 0 && w->n_heads > 0 && w->query_dim > 0;
+}
+
+int32_t shape_ok(const nrms_encoder_weights_t* w) {
+  if (!weights_ok(w)) return NRMS_ERR_INVALID_ARG;
+  if (w->d_model % w->n_heads != 0) return NRMS_ERR_INVALID_ARG;  // multihead_self.py:31
+  if (w->d_model / w->n_heads != kDK || w->n_heads != 15) return NRMS_ERR_UNSUPPORTED;
+  if (w->query_dim > kQMax || w->d_model % 4 != 0) return NRMS_ERR_UNSUPPORTED;
+  return NRMS_OK;
+}
+
+WeightRows qkv_rows(const nrms_encoder_weights_t* w) {
+  WeightRows r{};
+  r.w[0] = w->w_q; r.w[1] = w->w_k; r.w[2] = w->w_v;
+  r.b[0] = w->b_q; r.b[1] = w->b_k; r.b[2] = w->b_v;
+  r.seg_rows = w->d_model;
+  r.nseg = 3;
+  return r;
+}
+
+bool use_folded(int32_t mode, int64_t n_tok, int64_t V) {
+  if (mode == NRMS_PROJ_FOLDED) return true;
+  if (mode == NRMS_PROJ_DIRECT) return false;
+  return n_tok > V;
+}
+
+// Per-stage sizes (floats).
+struct NewsSizes {
+  size_t qkv, ctx, scores;
+};
+NewsSizes news_sizes(int64_t n_titles, int32_t L, int64_t V, int32_t D, bool folded) {
+  const size_t ntok = (size_t)n_titles * (size_t)L;
+  return {(folded ? (size_t)V : ntok) * 3 * (size_t)D, ntok * (size_t)D, ntok};
+}
+
+// attention + additive pooling from projected rows (shared by news and user paths)
+int32_t encode_from_qkv(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
+                        const int64_t* ids_b, int64_t n_seq, int32_t L,
+                        const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
+                        hipStream_t s) {
+  const int D = w->d_model;
+  int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
+  if (st) return st;
+  st = launch_gemm_additive_score(ctx, n_seq * L, D, w->w_add, w->b_add, w->q_add, w->query_dim,
+                                  scores, s);
+  if (st) return st;
+  return launch_additive_pool(ctx, scores, n_seq, L, D, out, s);
+}
+
+}  // namespace
+}  // namespace nrms
+
+using namespace nrms;
+
+extern "C" {
+
+int32_t nrms_abi_version(void) { return NRMS_ABI_VERSION; }
+
+const char* nrms_status_string(int32_t st) {
+  switch (st) {
+    case NRMS_OK: return "ok";
+    case NRMS_ERR_INVALID_ARG: return "invalid argument";
+    case NRMS_ERR_UNSUPPORTED: return "unsupported shape or alignment";
+    case NRMS_ERR_WORKSPACE: return "workspace missing or too small";
+    case NRMS_ERR_HIP: return "HIP launch failed";
+    default: return "unknown status";
+  }
+}
+
+int32_t nrms_last_hip_error(void) { return g_last_hip; }
+
+int32_t nrms_embedding_gather(const int64_t* ids, int64_t n_tok, const float* table, int64_t V,
+                              int32_t D, float* out, hipStream_t stream) {
+  if (n_tok < 0 || V < 0 || D <= 0) return NRMS_ERR_INVALID_ARG;
+  if (n_tok > 0 && (!ids || !table || !out)) return NRMS_ERR_INVALID_ARG;
+  return launch_gather(ids, n_tok, table, V, D, out, stream);
+}
+
+int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
+                         const nrms_encoder_weights_t* w, float* qkv, hipStream_t stream) {
+  if (M < 0 || n_rows_x < 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (M > 0 && (!x || !qkv)) return NRMS_ERR_INVALID_ARG;
+  const int D = w->d_model;
+  return launch_gemm_store(x, n_rows_x, row_ids, M, D, qkv_rows(w), 3 * D, qkv, 3 * D, stream);
+}
+
+int32_t nrms_self_attention(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
+                            int64_t n_seq_a, const int64_t* tok_ids_b, int64_t n_seq, int32_t L,
+                            const nrms_encoder_weights_t* w, float* ctx, hipStream_t stream) {
+  if (n_seq < 0 || n_seq_a < 0 || L <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (n_seq > 0 && (!qkv || !ctx)) return NRMS_ERR_INVALID_ARG;
+  return launch_mhsa(qkv, n_rows_qkv, tok_ids, n_seq_a, tok_ids_b, n_seq, L, w->n_heads, kDK, ctx,
+                     stream);
+}
+
+int32_t nrms_additive_attention(const float* x, int64_t n_seq, int32_t L,
+                                const nrms_encoder_weights_t* w, float* scores_ws, float* out,
+                                hipStream_t stream) {
+  if (n_seq < 0 || L <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (n_seq > 0 && (!x || !scores_ws || !out)) return NRMS_ERR_INVALID_ARG;
+  const int D = w->d_model;
+  int32_t st = launch_gemm_additive_score(x, n_seq * L, D, w->w_add, w->b_add, w->q_add,
+                                          w->query_dim, scores_ws, stream);
+  if (st) return st;
+  return launch_additive_pool(x, scores_ws, n_seq, L, D, out, stream);
+}
+
+int32_t nrms_additive_scores(const float* x, int64_t n_rows, const nrms_encoder_weights_t* w,
+                             float* scores, hipStream_t stream) {
+  if (n_rows < 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (n_rows > 0 && (!x || !scores)) return NRMS_ERR_INVALID_ARG;
+  return launch_gemm_additive_score(x, n_rows, w->d_model, w->w_add, w->b_add, w->q_add,
+                                    w->query_dim, scores, stream);
+}
+
+int32_t nrms_additive_pool(const float* x, const float* scores, int64_t n_seq, int32_t L,
+                           int32_t D, float* out, hipStream_t stream) {
+  if (n_seq < 0 || L <= 0 || D <= 0) return NRMS_ERR_INVALID_ARG;
+  if (n_seq > 0 && (!x || !scores || !out)) return NRMS_ERR_INVALID_ARG;
+  return launch_additive_pool(x, scores, n_seq, L, D, out, stream);
+}
+
+size_t nrms_news_encode_workspace_size(int64_t n_titles, int32_t L, int64_t V, int32_t D,
+                                       int32_t proj_mode) {
+  if (n_titles < 0 || L <= 0 || V < 0 || D <= 0) return 0;
+  const bool folded = use_folded(proj_mode, n_titles * L, V);
+  const NewsSizes z = news_sizes(n_titles, L, V, D, folded);
+  return align_up(z.qkv * 4) + align_up(z.ctx * 4) + align_up(z.scores * 4);
+}
+
+int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const float* table,
+                         int64_t V, const nrms_encoder_weights_t* w, int32_t proj_mode, float* out,
+                         void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  if (n_titles < 0 || L <= 0 || V <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (n_titles == 0) return NRMS_OK;
+  if (!ids || !table || !out) return NRMS_ERR_INVALID_ARG;
+  const int D = w->d_model;
+  const bool folded = use_folded(proj_mode, n_titles * L, V);
+  const NewsSizes z = news_sizes(n_titles, L, V, D, folded);
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* qkv = cv.floats(z.qkv);
+  float* ctx = cv.floats(z.ctx);
+  float* scores = cv.floats(z.scores);
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  int32_t st;
+  if (folded) {
+    // Vocabulary-level projection: one GEMM over the table, then rows gathered by id.
+    st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(w), 3 * D, qkv, 3 * D, stream);
+    if (st) return st;
+    return encode_from_qkv(qkv, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
+                           stream);
+  }
+  // Per-token projection with the embedding gather fused into the A-operand load.
+  st = launch_gemm_store(table, V, ids, n_titles * L, D, qkv_rows(w), 3 * D, qkv, 3 * D, stream);
+  if (st) return st;
+  return encode_from_qkv(qkv, n_titles * L, nullptr, n_titles, nullptr, n_titles, L, w, ctx,
+                         scores, out, stream);
+}
+
+size_t nrms_news_encode_folded_workspace_size(int64_t n_titles, int32_t L, int32_t D) {
+  if (n_titles < 0 || L <= 0 || D <= 0) return 0;
+  const size_t ntok = (size_t)n_titles * L;
+  return align_up(ntok * D * 4) + align_up(ntok * 4);
+}
+
+int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
+                                const float* qkv_table, int64_t V,
+                                const nrms_encoder_weights_t* w, float* out, void* workspace,
+                                size_t workspace_bytes, hipStream_t stream) {
+  if (n_titles < 0 || L <= 0 || V <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (n_titles == 0) return NRMS_OK;
+  if (!ids || !qkv_table || !out) return NRMS_ERR_INVALID_ARG;
+  const size_t ntok = (size_t)n_titles * L;
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* ctx = cv.floats(ntok * w->d_model);
+  float* scores = cv.floats(ntok);
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  return encode_from_qkv(qkv_table, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
+                         stream);
+}
+
+size_t nrms_user_encode_workspace_size(int64_t B, int32_t N, int32_t D) {
+  if (B < 0 || N <= 0 || D <= 0) return 0;
+  const size_t rows = (size_t)B * N;
+  return align_up(rows * 3 * D * 4) + align_up(rows * D * 4) + align_up(rows * 4);
+}
+
+int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N,
+                         const nrms_encoder_weights_t* w, float* out, void* workspace,
+                         size_t workspace_bytes, hipStream_t stream) {
+  if (B < 0 || N <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (B == 0) return NRMS_OK;
+  if (!clicked || !out) return NRMS_ERR_INVALID_ARG;
+  const int D = w->d_model;
+  const int64_t rows = B * N;
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* qkv = cv.floats((size_t)rows * 3 * D);
+  float* ctx = cv.floats((size_t)rows * D);
+  float* scores = cv.floats((size_t)rows);
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  int32_t st = launch_gemm_store(clicked, rows, nullptr, rows, D, qkv_rows(w), 3 * D, qkv, 3 * D,
+                                 stream);
+  if (st) return st;
+  return encode_from_qkv(qkv, rows, nullptr, B, nullptr, B, N, w, ctx, scores, out, stream);
+}
+
+int32_t nrms_score(const float* news, int64_t B, int32_t C, int64_t stride_b, int64_t stride_c,
+                   const float* user, int64_t stride_u, int32_t D, float* out,
+                   hipStream_t stream) {
+  if (B < 0 || C < 0 || D <= 0) return NRMS_ERR_INVALID_ARG;
+  if (B * C > 0 && (!news || !user || !out)) return NRMS_ERR_INVALID_ARG;
+  return launch_score(news, B, C, stride_b, stride_c, user, stride_u, D, out, stream);
+}
+
+size_t nrms_forward_workspace_size(int64_t B, int32_t C, int32_t N, int32_t L, int64_t V,
+                                   int32_t D, int32_t proj_mode) {
+  if (B < 0 || C < 0 || N <= 0 || L <= 0 || V < 0 || D <= 0) return 0;
+  const int64_t n_all = B * (C + N);
+  return nrms_news_encode_workspace_size(n_all, L, V, D, proj_mode) +
+         align_up((size_t)n_all * D * 4) + align_up((size_t)B * D * 4) +
+         nrms_user_encode_workspace_size(B, N, D);
+}
+
+int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_t B, int32_t C,
+                     int32_t N, int32_t L, const float* table, int64_t V,
+                     const nrms_encoder_weights_t* news_w, const nrms_encoder_weights_t* user_w,
+                     int32_t proj_mode, float* logits, void* workspace, size_t workspace_bytes,
+                     hipStream_t stream) {
+  if (B < 0 || C < 0 || N <= 0 || L <= 0 || V <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(news_w)) return st;
+  if (int32_t st = shape_ok(user_w)) return st;
+  if (news_w->d_model != user_w->d_model) return NRMS_ERR_INVALID_ARG;
+  if (B == 0) return NRMS_OK;
+  if (!cand_ids || !clicked_ids || !table || !logits) return NRMS_ERR_INVALID_ARG;
+  const int D = news_w->d_model;
+  const int64_t n_clk = B * N, n_all = B * (C + N);
+  const bool folded = use_folded(proj_mode, n_all * L, V);
+  const NewsSizes z = news_sizes(n_all, L, V, D, folded);
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* qkv = cv.floats(z.qkv);
+  float* ctx = cv.floats(z.ctx);
+  float* scores = cv.floats(z.scores);
+  float* news = cv.floats((size_t)n_all * D);   // [clicked B*N | candidates B*C] x D
+  float* user = cv.floats((size_t)B * D);
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  char* user_ws = static_cast<char*>(workspace) + cv.off;
+  const size_t user_ws_bytes = workspace_bytes - cv.off;
+
+  int32_t st;
+  if (folded) {
+    st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(news_w), 3 * D, qkv, 3 * D, stream);
+    if (st) return st;
+    st = encode_from_qkv(qkv, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores, news,
+                         stream);
+  } else {
+    st = launch_gemm_store(table, V, clicked_ids, n_clk * L, D, qkv_rows(news_w), 3 * D, qkv,
+                           3 * D, stream);
+    if (st) return st;
+    st = launch_gemm_store(table, V, cand_ids, B * C * L, D, qkv_rows(news_w), 3 * D,
+                           qkv + (size_t)n_clk * L * 3 * D, 3 * D, stream);
+    if (st) return st;
+    st = encode_from_qkv(qkv, n_all * L, nullptr, n_all, nullptr, n_all, L, news_w, ctx, scores,
+                         news, stream);
+  }
+  if (st) return st;
+  st = nrms_user_encode(news, B, N, user_w, user, user_ws, user_ws_bytes, stream);
+  if (st) return st;
+  return launch_score(news + (size_t)n_clk * D, B, C, (int64_t)C * D, D, user, D, D, logits,
+                      stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,222 @@
+// fp32 MFMA GEMM Y = X[row(m)] · W^T + b for the NRMS projections:
+//   * Q|K|V projection (multihead_self.py:53-58), N = 3D = 900, optional row
+//     indirection so the A operand can be gathered straight from the
+//     embedding table (DIRECT mode) or be the whole table (FOLDED mode);
+//   * additive-attention projection (additive.py:35-38), N = Q = 200, with the
+//     tanh(.)·q row reduction fused into the epilogue: the [rows, 200] tile
+//     never leaves registers, only one score per row is written.
+//
+// gfx950 specifics: v_mfma_f32_16x16x4_f32 (exact fp32, 256 FLOP/clk/CU);
+// 4 waves x (32 rows x 16·TN cols) per 128-row block; K staged through LDS in
+// 32-deep chunks with register prefetch of the next chunk; each lane reads
+// its A/B fragments with conflict-free ds_read_b64 (row stride 36 floats);
+// XCD-aware block order so the column tiles of one row tile share an L2.
+#include "nrms_common.hpp"
+
+namespace nrms {
+namespace {
+
+constexpr int BM = 128;
+constexpr int BK = 32;
+constexpr int LDS_LD = 36;  // floats; ≡ 4 (mod 64)/..: b64 fragment reads are conflict-free
+constexpr int kThreads = 256;
+
+// K-permutation: MFMA step (p, t) gives lane group kq (= lane >> 4) the K index
+// 8p + 2kq + t, so each lane fetches its two consecutive K values with one
+// ds_read_b64; A and B use the same map, so every K term is summed once.
+template <int TN, bool ADDITIVE>
+__global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
+    const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
+    int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy,
+    const float* __restrict__ qvec, float* __restrict__ score, int n_col_tiles) {
+  constexpr int BN = 16 * TN;
+  constexpr int A_PASSES = BM * BK / 4 / kThreads;              // 4
+  constexpr int B_PASSES = (BN * BK / 4 + kThreads - 1) / kThreads;
+  __shared__ __attribute__((aligned(16))) float As[BM * LDS_LD];
+  __shared__ __attribute__((aligned(16))) float Bs[BN * LDS_LD];
+
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int ct = wg % n_col_tiles;
+  const int64_t m0 = (int64_t)(wg / n_col_tiles) * BM;
+  const int n0 = ct * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int lrow = tid >> 3, lc4 = tid & 7;
+
+  // Staging sources: one A row and one W row per pass per thread.
+  const float* a_src[A_PASSES];
+  bool a_bad[A_PASSES];
+#pragma unroll
+  for (int p = 0; p < A_PASSES; ++p) {
+    const int64_t m = m0 + lrow + 32 * p;
+    a_src[p] = nullptr;
+    a_bad[p] = false;
+    if (m < M) {
+      const int64_t r = row_ids ? row_ids[m] : m;
+      if ((uint64_t)r < (uint64_t)n_rows_x) a_src[p] = X + r * K;
+      else a_bad[p] = true;  // invalid id: the row becomes NaN
+    }
+  }
+  const float* b_src[B_PASSES];
+#pragma unroll
+  for (int p = 0; p < B_PASSES; ++p) {
+    const int n = n0 + lrow + 32 * p;
+    b_src[p] = nullptr;
+    if (lrow + 32 * p < BN && n < N) {
+      const int seg = n / wr.seg_rows;
+      b_src[p] = wr.w[seg] + (int64_t)(n - seg * wr.seg_rows) * K;
+    }
+  }
+
+  float4 ra[A_PASSES], rb[B_PASSES];
+  auto gload = [&](int kc) {
+    const int k = kc * BK + lc4 * 4;
+    const bool kin = k < K;
+#pragma unroll
+    for (int p = 0; p < A_PASSES; ++p)
+      ra[p] = (a_src[p] && kin) ? *reinterpret_cast<const float4*>(a_src[p] + k)
+                                : (a_bad[p] ? nan4() : make_float4(0.f, 0.f, 0.f, 0.f));
+#pragma unroll
+    for (int p = 0; p < B_PASSES; ++p)
+      rb[p] = (b_src[p] && kin) ? *reinterpret_cast<const float4*>(b_src[p] + k)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int p = 0; p < A_PASSES; ++p)
+      *reinterpret_cast<float4*>(&As[(lrow + 32 * p) * LDS_LD + lc4 * 4]) = ra[p];
+#pragma unroll
+    for (int p = 0; p < B_PASSES; ++p)
+      if (lrow + 32 * p < BN)
+        *reinterpret_cast<float4*>(&Bs[(lrow + 32 * p) * LDS_LD + lc4 * 4]) = rb[p];
+  };
+
+  floatx4 acc[2][TN];
+#pragma unroll
+  for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) acc[ms][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int lm = lane & 15, kq = lane >> 4;
+  const float* Aw = As + (wave * 32 + lm) * LDS_LD + 2 * kq;
+  const float* Bw = Bs + lm * LDS_LD + 2 * kq;
+
+  const int nk = (K + BK - 1) / BK;
+  gload(0);
+  lstore();
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    if (kc + 1 < nk) gload(kc + 1);
+#pragma unroll
+    for (int p = 0; p < BK / 8; ++p) {
+      const float2 a0 = *reinterpret_cast<const float2*>(Aw + 8 * p);
+      const float2 a1 = *reinterpret_cast<const float2*>(Aw + 16 * LDS_LD + 8 * p);
+      float2 b[TN];
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn)
+        b[tn] = *reinterpret_cast<const float2*>(Bw + tn * 16 * LDS_LD + 8 * p);
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        acc[0][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b[tn].x, acc[0][tn], 0, 0, 0);
+        acc[1][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b[tn].x, acc[1][tn], 0, 0, 0);
+      }
+#pragma unroll
+      for (int tn = 0; tn < TN; ++tn) {
+        acc[0][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b[tn].y, acc[0][tn], 0, 0, 0);
+        acc[1][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b[tn].y, acc[1][tn], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (kc + 1 < nk) {
+      lstore();
+      __syncthreads();
+    }
+  }
+
+  // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
+  const int64_t row_base = m0 + wave * 32 + kq * 4;
+  if constexpr (!ADDITIVE) {
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int col = n0 + tn * 16 + lm;
+      if (col >= N) continue;
+      const int seg = col / wr.seg_rows;
+      const float bias = wr.b[seg][col - seg * wr.seg_rows];
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t row = row_base + ms * 16 + r;
+          if (row < M) Y[row * ldy + col] = acc[ms][tn][r] + bias;
+        }
+    }
+  } else {
+    float qv[TN], bv[TN];
+#pragma unroll
+    for (int tn = 0; tn < TN; ++tn) {
+      const int col = tn * 16 + lm;
+      qv[tn] = col < N ? qvec[col] : 0.f;
+      bv[tn] = col < N ? wr.b[0][col] : 0.f;
+    }
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float part = 0.f;
+#pragma unroll
+        for (int tn = 0; tn < TN; ++tn)
+          if (tn * 16 + lm < N) part = fmaf(qv[tn], tanhf(acc[ms][tn][r] + bv[tn]), part);
+        part += __shfl_xor(part, 1);
+        part += __shfl_xor(part, 2);
+        part += __shfl_xor(part, 4);
+        part += __shfl_xor(part, 8);
+        const int64_t row = row_base + ms * 16 + r;
+        if (lm == 0 && row < M) score[row] = part;
+      }
+  }
+}
+
+constexpr int TN_STORE = 12;     // BN = 192: N = 900 -> 5 column tiles
+constexpr int TN_ADDITIVE = 13;  // BN = 208 >= Q = 200: one column tile
+
+}  // namespace
+
+int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
+                          int K, const WeightRows& w, int N, float* Y, int64_t ldy,
+                          hipStream_t s) {
+  if (M == 0) return NRMS_OK;
+  if (K % 4 != 0 || ((uintptr_t)X % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  for (int i = 0; i < w.nseg; ++i)
+    if (((uintptr_t)w.w[i] % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  const int nct = (N + 16 * TN_STORE - 1) / (16 * TN_STORE);
+  const int64_t nrt = (M + BM - 1) / BM;
+  const int64_t blocks = nrt * nct;
+  if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, false>), dim3((unsigned)blocks),
+                     dim3(kThreads), 0, s, X, n_rows_x, row_ids, M, K, w, N, Y, ldy,
+                     (const float*)nullptr, (float*)nullptr, nct);
+  return launch_status();
+}
+
+int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
+                                   const float* b, const float* q, int N, float* score,
+                                   hipStream_t s) {
+  if (M == 0) return NRMS_OK;
+  if (N > 16 * TN_ADDITIVE) return NRMS_ERR_UNSUPPORTED;
+  if (K % 4 != 0 || ((uintptr_t)X % 16) != 0 || ((uintptr_t)W % 16) != 0)
+    return NRMS_ERR_UNSUPPORTED;
+  WeightRows w{};
+  w.w[0] = W;
+  w.b[0] = b;
+  w.seg_rows = N;
+  w.nseg = 1;
+  const int64_t blocks = (M + BM - 1) / BM;
+  if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_ADDITIVE, true>), dim3((unsigned)blocks),
+                     dim3(kThreads), 0, s, X, M, (const int64_t*)nullptr, M, K, w, N,
+                     (float*)nullptr, (int64_t)0, q, score, 1);
+  return launch_status();
+}
+
+}  // namespace nrms

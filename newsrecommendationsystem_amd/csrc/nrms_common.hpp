@@ -1,0 +1,85 @@
+// Shared device helpers and launch plumbing for libnrms_hip.so (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "nrms_hip.h"
+
+namespace nrms {
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;  // CDNA wavefront
+
+// Remember the last HIP failure per host thread (nrms_last_hip_error()).
+void set_last_hip_error(hipError_t e);
+
+inline int32_t launch_status() {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_last_hip_error(e);
+    return NRMS_ERR_HIP;
+  }
+  return NRMS_OK;
+}
+
+__device__ __forceinline__ float qnan() { return __builtin_nanf(""); }
+
+__device__ __forceinline__ float4 nan4() {
+  const float n = qnan();
+  return make_float4(n, n, n, n);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// max that propagates NaN (torch.max semantics): any NaN lane -> NaN.
+__device__ __forceinline__ float nan_max(float a, float b) {
+  return (a != a || b != b) ? qnan() : fmaxf(a, b);
+}
+
+__device__ __forceinline__ float wave_max_nan(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = nan_max(v, __shfl_xor(v, o));
+  return v;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5, "XCD swizzle
+// must be bijective"): blocks dealt round-robin over 8 XCDs get contiguous
+// logical ids per XCD, so tiles that share operands share an L2.
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// Row segments of a stacked weight W[N, K] = [W_0; W_1; W_2] with biases
+// (the Q|K|V projection is three nn.Linear weights used as one N = 3D GEMM).
+struct WeightRows {
+  const float* w[3];
+  const float* b[3];
+  int seg_rows;
+  int nseg;
+};
+
+// Host-side launchers (defined in the .hip files).
+int32_t launch_gather(const int64_t* ids, int64_t n_tok, const float* table, int64_t V, int D,
+                      float* out, hipStream_t s);
+int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
+                          int K, const WeightRows& w, int N, float* Y, int64_t ldy,
+                          hipStream_t s);
+int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
+                                   const float* b, const float* q, int N, float* score,
+                                   hipStream_t s);
+int32_t launch_mhsa(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
+                    const int64_t* ids_b, int64_t n_seq, int L, int H, int DK, float* ctx,
+                    hipStream_t s);
+int32_t launch_additive_pool(const float* x, const float* score, int64_t n_seq, int L, int D,
+                             float* out, hipStream_t s);
+int32_t launch_score(const float* news, int64_t B, int C, int64_t sb, int64_t sc,
+                     const float* user, int64_t su, int D, float* out, hipStream_t s);
+
+}  // namespace nrms

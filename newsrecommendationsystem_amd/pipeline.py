@@ -1,0 +1,120 @@
+"""Stage-by-stage NRMS forward over the C ABI, with optional HIP-event timing.
+
+``nrms_forward`` (include/nrms_hip.h) runs the whole scoring path in one call;
+ForwardPlan issues the same launches one stage at a time from preallocated
+buffers so a harness can bracket each kernel with events on the launch stream
+(bench.py uses this for the per-kernel roofline). Output is bitwise identical
+to nrms_forward (tests/test_gpu_parity.py::test_plan_matches_forward).
+
+Stage order (forward semantics, src/model/NRMS/__init__.py:19-48):
+  qkv_news      Q|K|V projection (folded: whole vocabulary; direct: every token)
+  mhsa_news     raw-exp self-attention of all B*(N+C) titles
+  addscore_news additive-attention token scores (GEMM + tanh·q epilogue)
+  pool_news     softmax over L + weighted sum -> news vectors
+  qkv_user / mhsa_user / addscore_user / pool_user   the UserEncoder
+  score         dot-product click predictor
+"""
+import ctypes
+
+import torch
+
+from . import _native as N
+
+D_MODEL = 300
+
+
+class ForwardPlan:
+    def __init__(self, model, B, C, n_clicked, L, proj_mode=N.NRMS_PROJ_FOLDED):
+        ne = model.news_encoder
+        self.model = model
+        self.dev = ne.word_embedding.weight.device
+        self.table = ne.table()
+        self.V, self.D = self.table.shape
+        self.B, self.C, self.N, self.L = B, C, n_clicked, L
+        n_all = B * (C + n_clicked)
+        self.folded = proj_mode == N.NRMS_PROJ_FOLDED or (
+            proj_mode == N.NRMS_PROJ_AUTO and n_all * L > self.V)
+        f32 = dict(dtype=torch.float32, device=self.dev)
+        D = self.D
+        qkv_rows = self.V if self.folded else n_all * L
+        self.qkv = torch.empty(qkv_rows, 3 * D, **f32)
+        self.ctx = torch.empty(n_all * L, D, **f32)
+        self.scores = torch.empty(n_all * L, **f32)
+        self.news = torch.empty(n_all, D, **f32)        # [clicked B*N | candidates B*C]
+        self.uqkv = torch.empty(B * n_clicked, 3 * D, **f32)
+        self.uctx = torch.empty(B * n_clicked, D, **f32)
+        self.uscores = torch.empty(B * n_clicked, **f32)
+        self.user = torch.empty(B, D, **f32)
+        self.logits = torch.empty(B, C, **f32)
+        self.wn, self._keep_n = ne.weights()
+        self.wu, self._keep_u = model.user_encoder.weights()
+        self.stages = ["qkv_news", "mhsa_news", "addscore_news", "pool_news", "qkv_user",
+                       "mhsa_user", "addscore_user", "pool_user", "score"]
+
+    def run(self, cand_ids, clicked_ids, events=None):
+        """cand_ids [B,C,L], clicked_ids [B,N,L] int64 on the device. If
+        ``events`` (len(stages)+1 torch.cuda.Event) is given, event i is
+        recorded before stage i and the last one after the final stage."""
+        B, C, Nc, L, D, V = self.B, self.C, self.N, self.L, self.D, self.V
+        n_clk, n_all = B * Nc, B * (C + Nc)
+        st = N.stream_handle(self.dev)
+        wn, wu = ctypes.byref(self.wn), ctypes.byref(self.wu)
+        P = N.ptr
+        rec = (lambda i: events[i].record()) if events is not None else (lambda i: None)
+
+        rec(0)
+        if self.folded:
+            N.call("nrms_qkv_project", P(self.table), V, None, V, wn, P(self.qkv), st)
+        else:
+            N.call("nrms_qkv_project", P(self.table), V, P(clicked_ids), n_clk * L, wn,
+                   P(self.qkv), st)
+            tail = self.qkv[n_clk * L:]
+            N.call("nrms_qkv_project", P(self.table), V, P(cand_ids), B * C * L, wn, P(tail), st)
+        rec(1)
+        if self.folded:
+            N.call("nrms_self_attention", P(self.qkv), V, P(clicked_ids), n_clk, P(cand_ids),
+                   n_all, L, wn, P(self.ctx), st)
+        else:
+            N.call("nrms_self_attention", P(self.qkv), n_all * L, None, n_all, None, n_all, L, wn,
+                   P(self.ctx), st)
+        rec(2)
+        N.call("nrms_additive_scores", P(self.ctx), n_all * L, wn, P(self.scores), st)
+        rec(3)
+        N.call("nrms_additive_pool", P(self.ctx), P(self.scores), n_all, L, D, P(self.news), st)
+        rec(4)
+        N.call("nrms_qkv_project", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), st)
+        rec(5)
+        N.call("nrms_self_attention", P(self.uqkv), n_clk, None, B, None, B, Nc, wu,
+               P(self.uctx), st)
+        rec(6)
+        N.call("nrms_additive_scores", P(self.uctx), n_clk, wu, P(self.uscores), st)
+        rec(7)
+        N.call("nrms_additive_pool", P(self.uctx), P(self.uscores), B, Nc, D, P(self.user), st)
+        rec(8)
+        N.call("nrms_score", P(self.news[n_clk:]), B, C, C * D, D, P(self.user), D, D,
+               P(self.logits), st)
+        rec(9)
+        return self.logits
+
+    # Algorithmic work per launch of each stage (SURVEY §8d conventions:
+    # GEMMs 2·M·N·K; bytes = operands the stage must read + results it writes).
+    def work(self):
+        B, C, Nc, L, D, V = self.B, self.C, self.N, self.L, self.D, self.V
+        Q, H, dk = 200, 15, D // 15
+        n_all, n_clk = B * (C + Nc), B * Nc
+        att_flop = lambda seqs, l: seqs * H * 2 * (2 * l * l * dk)
+        qkv_m = V if self.folded else n_all * L
+        return {
+            "qkv_news": dict(flop=2 * qkv_m * D * 3 * D,
+                             bytes=4 * (qkv_m * D + qkv_m * 3 * D + 3 * D * D)),
+            # gathered q|k|v rows + ids + context rows written
+            "mhsa_news": dict(flop=att_flop(n_all, L),
+                              bytes=n_all * L * (4 * 3 * D + (8 if self.folded else 0) + 4 * D)),
+            "addscore_news": dict(flop=2 * n_all * L * D * Q, bytes=4 * (n_all * L * (D + 1) + Q * D)),
+            "pool_news": dict(flop=2 * n_all * L * D, bytes=4 * (n_all * L * (D + 1) + n_all * D)),
+            "qkv_user": dict(flop=2 * n_clk * D * 3 * D, bytes=4 * (n_clk * 4 * D + 3 * D * D)),
+            "mhsa_user": dict(flop=att_flop(B, Nc), bytes=4 * n_clk * 4 * D),
+            "addscore_user": dict(flop=2 * n_clk * D * Q, bytes=4 * (n_clk * (D + 1) + Q * D)),
+            "pool_user": dict(flop=2 * n_clk * D, bytes=4 * (n_clk * (D + 1) + B * D)),
+            "score": dict(flop=2 * B * C * D, bytes=4 * (B * C * D + B * D + B * C)),
+        }
