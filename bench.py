@@ -72,7 +72,7 @@ def load_traffic(kernel):
         return None
 
 
-def cpu_baseline(model, device, sample_B=32, min_seconds=10.0, max_reps=5):
+def cpu_baseline(model, device, sample_B=32, min_seconds=12.0, max_reps=500):
     """Time the oracle's ATen-order CPU restatement (oracle/nrms_torch_cpu.py)
     on a bounded sample of the same workload; also check GPU parity on it."""
     from oracle import nrms_torch_cpu as T

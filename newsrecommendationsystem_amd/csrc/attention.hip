@@ -137,17 +137,23 @@ __global__ __launch_bounds__(kPoolThreads) void additive_pool_kernel(
   const int d4 = D / 4;
   const float4* xs = reinterpret_cast<const float4*>(x + s * L * D);
   float4* os = reinterpret_cast<float4*>(out + s * D);
-  for (int c = lane; c < d4; c += kWave) {
+  // The shuffle must run with every lane active (a bpermute from an inactive
+  // lane reads garbage), so the column guard sits inside the l-loop.
+  for (int c0 = 0; c0 < d4; c0 += kWave) {
+    const int c = c0 + lane;
+    const bool live = c < d4;
     float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int l = 0; l < L; ++l) {
       const float wl = __shfl(w, l);
-      const float4 xv = xs[l * d4 + c];
-      acc.x = fmaf(wl, xv.x, acc.x);
-      acc.y = fmaf(wl, xv.y, acc.y);
-      acc.z = fmaf(wl, xv.z, acc.z);
-      acc.w = fmaf(wl, xv.w, acc.w);
+      if (live) {
+        const float4 xv = xs[l * d4 + c];
+        acc.x = fmaf(wl, xv.x, acc.x);
+        acc.y = fmaf(wl, xv.y, acc.y);
+        acc.z = fmaf(wl, xv.z, acc.z);
+        acc.w = fmaf(wl, xv.w, acc.w);
+      }
     }
-    os[c] = acc;
+    if (live) os[c] = acc;
   }
 }
 

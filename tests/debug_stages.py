@@ -1,0 +1,111 @@
+"""Ad-hoc stage-by-stage diagnosis of the HIP path against numpy (run on a GPU box):
+    python tests/debug_stages.py
+Prints the normwise relative error of every stage given exact inputs."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from newsrecommendationsystem_amd import NRMS, NRMSConfig  # noqa: E402
+from newsrecommendationsystem_amd import _native as N  # noqa: E402
+from oracle import nrms_oracle as O  # noqa: E402
+from oracle import weights as W  # noqa: E402
+
+
+def rel(a, b):
+    a = np.asarray(a, np.float64).reshape(len(a), -1)
+    b = np.asarray(b, np.float64).reshape(len(b), -1)
+    return float((np.linalg.norm(a - b, axis=1) / np.maximum(np.linalg.norm(b, axis=1), 1e-30)).max())
+
+
+def main():
+    dev = torch.device("cuda:0")
+    V = 256
+    sd = W.nrms_state(20251015, V)
+
+    class Cfg(NRMSConfig):
+        num_words = V
+    m = NRMS(Cfg)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.to(dev).eval()
+    ne = m.news_encoder
+    ids_np = W.titles(1, 2, 16, V)
+    ids = torch.from_numpy(ids_np).to(dev)
+    n, L = ids.shape
+    tab = ne.table()
+    w, keep = ne.weights()
+    st = N.stream_handle(dev)
+    P = N.ptr
+
+    # plain GEMM check with structured data: X = arange pattern, W identity-ish
+    qkv = torch.empty(n * L, 900, device=dev)
+    N.call("nrms_qkv_project", P(tab), V, P(ids), n * L, ctypes.byref(w), P(qkv), st)
+    torch.cuda.synchronize()
+    x = sd["news_encoder.word_embedding.weight"][ids_np].reshape(-1, 300)
+    p = "news_encoder.multihead_self_attention"
+    ref_qkv = np.concatenate([O.linear(x, sd[f"{p}.{k}.weight"], sd[f"{p}.{k}.bias"], np.float64)
+                              for k in ("W_Q", "W_K", "W_V")], axis=1)
+    got = qkv.cpu().numpy()
+    print("qkv rel", rel(got, ref_qkv))
+    bad = np.abs(got - ref_qkv) > 1e-3 * np.abs(ref_qkv).max()
+    print("bad frac", bad.mean(), "bad rows", np.unique(np.where(bad)[0])[:20], "bad cols", np.unique(np.where(bad)[1])[:40])
+
+    # identity GEMM test: W = I (3 segs), b = 0, X = structured
+    eye = torch.eye(300, device=dev)
+    zb = torch.zeros(300, device=dev)
+    w2 = N.EncoderWeights(eye.data_ptr(), zb.data_ptr(), eye.data_ptr(), zb.data_ptr(), eye.data_ptr(), zb.data_ptr(),
+                          keep[6].data_ptr(), keep[7].data_ptr(), keep[8].data_ptr(), 300, 15, 200)
+    X = (torch.arange(300 * 256, device=dev, dtype=torch.float32).view(256, 300) % 97) / 97.0
+    Y = torch.empty(256, 900, device=dev)
+    N.call("nrms_qkv_project", P(X), 256, None, 256, ctypes.byref(w2), P(Y), st)
+    torch.cuda.synchronize()
+    Yn = Y.cpu().numpy()
+    Xn = X.cpu().numpy()
+    print("identity GEMM max err", np.abs(Yn[:, :300] - Xn).max(), np.abs(Yn[:, 300:600] - Xn).max())
+    diff = np.abs(Yn[:, :300] - Xn) > 1e-6
+    if diff.any():
+        r, c = np.where(diff)
+        print("first bad (row,col)", list(zip(r[:10], c[:10])))
+        print("got", Yn[r[0], c[0]], "want", Xn[r[0], c[0]])
+        # find which X element it equals
+        hits = np.argwhere(np.abs(Xn - Yn[r[0], c[0]]) < 1e-7)
+        print("value found at", hits[:5])
+
+    # mhsa given exact qkv (from reference projection)
+    qkv_ref_t = torch.from_numpy(ref_qkv.astype(np.float32)).to(dev)
+    ctx = torch.empty(n * L, 300, device=dev)
+    N.call("nrms_self_attention", P(qkv_ref_t), n * L, None, n, None, n, L, ctypes.byref(w), P(ctx), st)
+    torch.cuda.synchronize()
+    q = ref_qkv[:, :300].reshape(n, L, 15, 20).transpose(0, 2, 1, 3)
+    k = ref_qkv[:, 300:600].reshape(n, L, 15, 20).transpose(0, 2, 1, 3)
+    v = ref_qkv[:, 600:].reshape(n, L, 15, 20).transpose(0, 2, 1, 3)
+    ctx_ref = O.raw_exp_attention(q, k, v, 20, np.float64).transpose(0, 2, 1, 3).reshape(n * L, 300)
+    print("mhsa rel", rel(ctx.cpu().numpy(), ctx_ref))
+
+    # additive scores given exact ctx
+    ctx_t = torch.from_numpy(ctx_ref.astype(np.float32)).to(dev)
+    sc = torch.empty(n * L, device=dev)
+    N.call("nrms_additive_scores", P(ctx_t), n * L, ctypes.byref(w), P(sc), st)
+    torch.cuda.synchronize()
+    pa = "news_encoder.additive_attention"
+    t = np.tanh(O.linear(ctx_ref, sd[f"{pa}.linear.weight"], sd[f"{pa}.linear.bias"], np.float64))
+    sc_ref = t @ sd[f"{pa}.attention_query_vector"].astype(np.float64)
+    print("scores max abs err", np.abs(sc.cpu().numpy() - sc_ref).max(), "scale", np.abs(sc_ref).max())
+
+    # pool given exact scores
+    sc_t = torch.from_numpy(sc_ref.astype(np.float32)).to(dev)
+    out = torch.empty(n, 300, device=dev)
+    N.call("nrms_additive_pool", P(ctx_t), P(sc_t), n, L, 300, P(out), st)
+    torch.cuda.synchronize()
+    s2 = sc_ref.reshape(n, L)
+    e = np.exp(s2 - s2.max(1, keepdims=True))
+    wgt = e / e.sum(1, keepdims=True)
+    out_ref = np.einsum("nl,nld->nd", wgt, ctx_ref.reshape(n, L, 300))
+    print("pool rel", rel(out.cpu().numpy(), out_ref))
+
+
+if __name__ == "__main__":
+    main()
