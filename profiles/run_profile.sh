@@ -1,0 +1,17 @@
+#!/usr/bin/env bash
+# Profile the bench workload on a GPU box (run from the repo root via gpurun):
+#   bash profiles/run_profile.sh <tag>
+# 1) kernel trace + stats (per-kernel durations), 2) FETCH_SIZE pass,
+# 3) WRITE_SIZE pass (separate passes: TCC slots; never combined with
+# sys/runtime traces). Outputs land in gpurun_out/prof_<tag>/.
+set -euo pipefail
+TAG=${1:-r01}
+REPO=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$REPO/gpurun_out/prof_$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+BENCH=("$REPO/bench.py" --steps 20 --warmup 5 --no-cpu-baseline)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" > "$OUT/bench_trace.json"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "${BENCH[@]}" > "$OUT/bench_fetch.json"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 "${BENCH[@]}" > "$OUT/bench_write.json"
+find "$OUT" -name '*.csv' | sort
