@@ -107,6 +107,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1024, help="impressions per GPU per step")
     ap.add_argument("--proj", choices=["folded", "direct", "auto"], default="folded")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--unfused", action="store_true", help="separate MHSA / additive / pool kernels")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -128,7 +129,7 @@ def main():
     model = build_model(device)
     B = args.batch
     cand, clk = synth_impressions(1000 + rank, B, V_WORDS, device)   # this rank's user shard
-    plan = ForwardPlan(model, B, C, N_CLICKED, L, proj_mode=mode)
+    plan = ForwardPlan(model, B, C, N_CLICKED, L, proj_mode=mode, fused=not args.unfused)
     n_st = len(plan.stages)
 
     with torch.no_grad():
@@ -183,7 +184,8 @@ def main():
                                "click predictor), every title encoded", "global_batch": B * world,
                    "impressions_per_gpu": B, "candidates": C, "clicked": N_CLICKED,
                    "title_len": L, "vocab": V_WORDS, "d_model": D, "heads": 15,
-                   "query_dim": 200, "proj_mode": args.proj, "parallelism": f"user-shard x{world}"},
+                   "query_dim": 200, "proj_mode": args.proj, "news_tail": "unfused" if args.unfused else "fused",
+                   "parallelism": f"user-shard x{world}"},
         "roofline": {"kernel": dom, "bound": bound, "achieved": round(achieved, 3),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
                      "traffic": load_traffic(dom),

@@ -109,6 +109,18 @@ int32_t nrms_additive_scores(const float* x, int64_t n_rows, const nrms_encoder_
 int32_t nrms_additive_pool(const float* x, const float* scores, int64_t n_seq, int32_t L,
                            int32_t D, float* out, hipStream_t stream);
 
+/* Fused NewsEncoder tail (news_encoder.py:42-47): raw-exp MHSA over projected
+ * rows + additive attention + pooling, 4 titles per workgroup, the context
+ * consumed from LDS by the additive GEMM. Row addressing as
+ * nrms_self_attention. Compiled for the reference geometry (L = 20, D = 300,
+ * H = 15, Q = 200); other shapes return NRMS_ERR_UNSUPPORTED (use the stage
+ * entry points). Used by nrms_news_encode* and nrms_forward when it applies. */
+size_t nrms_news_attention_pool_workspace_size(int64_t n_titles, int32_t L, int32_t D);
+int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
+                                 int64_t n_seq_a, const int64_t* tok_ids_b, int64_t n_titles,
+                                 int32_t L, const nrms_encoder_weights_t* w, float* out,
+                                 void* workspace, size_t workspace_bytes, hipStream_t stream);
+
 /* NewsEncoder.forward (src/model/NRMS/news_encoder.py:27-48), eval mode:
  * ids[n_titles, L] -> out[n_titles, D]. */
 size_t nrms_news_encode_workspace_size(int64_t n_titles, int32_t L, int64_t V, int32_t D,

@@ -42,6 +42,8 @@ SIGNATURES = {
     "nrms_additive_attention": (_i32, [_p, _i64, _i32, _EW, _p, _p, _p]),
     "nrms_additive_scores": (_i32, [_p, _i64, _EW, _p, _p]),
     "nrms_additive_pool": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),
+    "nrms_news_attention_pool_workspace_size": (_sz, [_i64, _i32, _i32]),
+    "nrms_news_attention_pool": (_i32, [_p, _i64, _p, _i64, _p, _i64, _i32, _EW, _p, _p, _sz, _p]),
     "nrms_news_encode_workspace_size": (_sz, [_i64, _i32, _i64, _i32, _i32]),
     "nrms_news_encode": (_i32, [_p, _i64, _i32, _p, _i64, _EW, _i32, _p, _p, _sz, _p]),
     "nrms_news_encode_folded_workspace_size": (_sz, [_i64, _i32, _i32]),

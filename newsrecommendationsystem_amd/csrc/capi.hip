@@ -62,19 +62,27 @@ bool use_folded(int32_t mode, int64_t n_tok, int64_t V) {
 
 // Per-stage sizes (floats).
 struct NewsSizes {
-  size_t qkv, ctx, scores;
+  size_t qkv, ctx, scores, wap;
 };
 NewsSizes news_sizes(int64_t n_titles, int32_t L, int64_t V, int32_t D, bool folded) {
   const size_t ntok = (size_t)n_titles * (size_t)L;
-  return {(folded ? (size_t)V : ntok) * 3 * (size_t)D, ntok * (size_t)D, ntok};
+  return {(folded ? (size_t)V : ntok) * 3 * (size_t)D, ntok * (size_t)D, ntok,
+          fused_news_packed_b_floats()};
+}
+size_t news_bytes(const NewsSizes& z) {
+  return align_up(z.qkv * 4) + align_up(z.ctx * 4) + align_up(z.scores * 4) + align_up(z.wap * 4);
 }
 
-// attention + additive pooling from projected rows (shared by news and user paths)
+// attention + additive pooling from projected rows (shared by news and user
+// paths). `wap` non-null: use the fused news kernel when the geometry allows.
 int32_t encode_from_qkv(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
                         const int64_t* ids_b, int64_t n_seq, int32_t L,
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
-                        hipStream_t s) {
+                        hipStream_t s, float* wap = nullptr) {
   const int D = w->d_model;
+  if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
+    return launch_fused_news(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
+                             w->q_add, wap, ctx, out, s);
   int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
   st = launch_gemm_additive_score(ctx, n_seq * L, D, w->w_add, w->b_add, w->q_add, w->query_dim,
@@ -160,12 +168,33 @@ int32_t nrms_additive_pool(const float* x, const float* scores, int64_t n_seq, i
   return launch_additive_pool(x, scores, n_seq, L, D, out, stream);
 }
 
+size_t nrms_news_attention_pool_workspace_size(int64_t n_titles, int32_t L, int32_t D) {
+  if (n_titles < 0 || L <= 0 || D <= 0) return 0;
+  return align_up((size_t)n_titles * L * D * 4) + align_up(fused_news_packed_b_floats() * 4);
+}
+
+int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
+                                 int64_t n_seq_a, const int64_t* tok_ids_b, int64_t n_titles,
+                                 int32_t L, const nrms_encoder_weights_t* w, float* out,
+                                 void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  if (n_titles < 0 || n_seq_a < 0 || L <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (!fused_news_supported(L, w->d_model, w->n_heads, w->query_dim)) return NRMS_ERR_UNSUPPORTED;
+  if (n_titles == 0) return NRMS_OK;
+  if (!qkv || !out) return NRMS_ERR_INVALID_ARG;
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* ctx = cv.floats((size_t)n_titles * L * w->d_model);
+  float* wap = cv.floats(fused_news_packed_b_floats());
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  return launch_fused_news(qkv, n_rows_qkv, tok_ids, n_seq_a, tok_ids_b, n_titles, w->w_add,
+                           w->b_add, w->q_add, wap, ctx, out, stream);
+}
+
 size_t nrms_news_encode_workspace_size(int64_t n_titles, int32_t L, int64_t V, int32_t D,
                                        int32_t proj_mode) {
   if (n_titles < 0 || L <= 0 || V < 0 || D <= 0) return 0;
   const bool folded = use_folded(proj_mode, n_titles * L, V);
-  const NewsSizes z = news_sizes(n_titles, L, V, D, folded);
-  return align_up(z.qkv * 4) + align_up(z.ctx * 4) + align_up(z.scores * 4);
+  return news_bytes(news_sizes(n_titles, L, V, D, folded));
 }
 
 int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const float* table,
@@ -182,6 +211,7 @@ int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const 
   float* qkv = cv.floats(z.qkv);
   float* ctx = cv.floats(z.ctx);
   float* scores = cv.floats(z.scores);
+  float* wap = cv.floats(z.wap);
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   int32_t st;
   if (folded) {
@@ -189,19 +219,19 @@ int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const 
     st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(w), 3 * D, qkv, 3 * D, stream);
     if (st) return st;
     return encode_from_qkv(qkv, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
-                           stream);
+                           stream, wap);
   }
   // Per-token projection with the embedding gather fused into the A-operand load.
   st = launch_gemm_store(table, V, ids, n_titles * L, D, qkv_rows(w), 3 * D, qkv, 3 * D, stream);
   if (st) return st;
   return encode_from_qkv(qkv, n_titles * L, nullptr, n_titles, nullptr, n_titles, L, w, ctx,
-                         scores, out, stream);
+                         scores, out, stream, wap);
 }
 
 size_t nrms_news_encode_folded_workspace_size(int64_t n_titles, int32_t L, int32_t D) {
   if (n_titles < 0 || L <= 0 || D <= 0) return 0;
   const size_t ntok = (size_t)n_titles * L;
-  return align_up(ntok * D * 4) + align_up(ntok * 4);
+  return align_up(ntok * D * 4) + align_up(ntok * 4) + align_up(fused_news_packed_b_floats() * 4);
 }
 
 int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
@@ -216,9 +246,10 @@ int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
   float* ctx = cv.floats(ntok * w->d_model);
   float* scores = cv.floats(ntok);
+  float* wap = cv.floats(fused_news_packed_b_floats());
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   return encode_from_qkv(qkv_table, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
-                         stream);
+                         stream, wap);
 }
 
 size_t nrms_user_encode_workspace_size(int64_t B, int32_t N, int32_t D) {
@@ -283,6 +314,7 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   float* qkv = cv.floats(z.qkv);
   float* ctx = cv.floats(z.ctx);
   float* scores = cv.floats(z.scores);
+  float* wap = cv.floats(z.wap);
   float* news = cv.floats((size_t)n_all * D);   // [clicked B*N | candidates B*C] x D
   float* user = cv.floats((size_t)B * D);
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
@@ -294,7 +326,7 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
     st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(news_w), 3 * D, qkv, 3 * D, stream);
     if (st) return st;
     st = encode_from_qkv(qkv, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores, news,
-                         stream);
+                         stream, wap);
   } else {
     st = launch_gemm_store(table, V, clicked_ids, n_clk * L, D, qkv_rows(news_w), 3 * D, qkv,
                            3 * D, stream);
@@ -303,7 +335,7 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
                            qkv + (size_t)n_clk * L * 3 * D, 3 * D, stream);
     if (st) return st;
     st = encode_from_qkv(qkv, n_all * L, nullptr, n_all, nullptr, n_all, L, news_w, ctx, scores,
-                         news, stream);
+                         news, stream, wap);
   }
   if (st) return st;
   st = nrms_user_encode(news, B, N, user_w, user, user_ws, user_ws_bytes, stream);

@@ -79,6 +79,12 @@ int32_t launch_mhsa(const float* qkv, int64_t n_rows, const int64_t* ids_a, int6
                     hipStream_t s);
 int32_t launch_additive_pool(const float* x, const float* score, int64_t n_seq, int L, int D,
                              float* out, hipStream_t s);
+size_t fused_news_packed_b_floats();
+bool fused_news_supported(int L, int D, int H, int Q);
+int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
+                          const int64_t* ids_b, int64_t n_titles, const float* w_add,
+                          const float* b_add, const float* q_add, float* wap, float* ctx,
+                          float* out, hipStream_t s);
 int32_t launch_score(const float* news, int64_t B, int C, int64_t sb, int64_t sc,
                      const float* user, int64_t su, int D, float* out, hipStream_t s);
 

@@ -8,9 +8,10 @@ to nrms_forward (tests/test_gpu_parity.py::test_plan_matches_forward).
 
 Stage order (forward semantics, src/model/NRMS/__init__.py:19-48):
   qkv_news      Q|K|V projection (folded: whole vocabulary; direct: every token)
-  mhsa_news     raw-exp self-attention of all B*(N+C) titles
-  addscore_news additive-attention token scores (GEMM + tanh·q epilogue)
-  pool_news     softmax over L + weighted sum -> news vectors
+  news_fused    raw-exp MHSA + additive attention + pooling of all B*(N+C)
+                titles in one kernel (nrms_news_attention_pool); with
+                fused=False the three separate stages instead:
+                mhsa_news / addscore_news / pool_news
   qkv_user / mhsa_user / addscore_user / pool_user   the UserEncoder
   score         dot-product click predictor
 """
@@ -24,7 +25,7 @@ D_MODEL = 300
 
 
 class ForwardPlan:
-    def __init__(self, model, B, C, n_clicked, L, proj_mode=N.NRMS_PROJ_FOLDED):
+    def __init__(self, model, B, C, n_clicked, L, proj_mode=N.NRMS_PROJ_FOLDED, fused=True):
         ne = model.news_encoder
         self.model = model
         self.dev = ne.word_embedding.weight.device
@@ -48,8 +49,13 @@ class ForwardPlan:
         self.logits = torch.empty(B, C, **f32)
         self.wn, self._keep_n = ne.weights()
         self.wu, self._keep_u = model.user_encoder.weights()
-        self.stages = ["qkv_news", "mhsa_news", "addscore_news", "pool_news", "qkv_user",
-                       "mhsa_user", "addscore_user", "pool_user", "score"]
+        self.fused = fused
+        news_st = ["news_fused"] if fused else ["mhsa_news", "addscore_news", "pool_news"]
+        self.stages = ["qkv_news"] + news_st + ["qkv_user", "mhsa_user", "addscore_user",
+                                                "pool_user", "score"]
+        if fused:
+            nb = N.load().nrms_news_attention_pool_workspace_size(n_all, L, D)
+            self.fws = torch.empty(nb, dtype=torch.uint8, device=self.dev)
 
     def run(self, cand_ids, clicked_ids, events=None):
         """cand_ids [B,C,L], clicked_ids [B,N,L] int64 on the device. If
@@ -71,29 +77,33 @@ class ForwardPlan:
             tail = self.qkv[n_clk * L:]
             N.call("nrms_qkv_project", P(self.table), V, P(cand_ids), B * C * L, wn, P(tail), st)
         rec(1)
-        if self.folded:
-            N.call("nrms_self_attention", P(self.qkv), V, P(clicked_ids), n_clk, P(cand_ids),
-                   n_all, L, wn, P(self.ctx), st)
+        k = 1
+        rows, ia, ib = (V, P(clicked_ids), P(cand_ids)) if self.folded else (n_all * L, None, None)
+        if self.fused:
+            N.call("nrms_news_attention_pool", P(self.qkv), rows, ia, n_clk, ib, n_all, L, wn,
+                   P(self.news), P(self.fws), self.fws.numel(), st)
         else:
-            N.call("nrms_self_attention", P(self.qkv), n_all * L, None, n_all, None, n_all, L, wn,
+            N.call("nrms_self_attention", P(self.qkv), rows, ia, n_clk, ib, n_all, L, wn,
                    P(self.ctx), st)
-        rec(2)
-        N.call("nrms_additive_scores", P(self.ctx), n_all * L, wn, P(self.scores), st)
-        rec(3)
-        N.call("nrms_additive_pool", P(self.ctx), P(self.scores), n_all, L, D, P(self.news), st)
-        rec(4)
+            rec(k + 1)
+            N.call("nrms_additive_scores", P(self.ctx), n_all * L, wn, P(self.scores), st)
+            rec(k + 2)
+            N.call("nrms_additive_pool", P(self.ctx), P(self.scores), n_all, L, D, P(self.news), st)
+            k += 2
+        k += 1
+        rec(k)
         N.call("nrms_qkv_project", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), st)
-        rec(5)
+        rec(k + 1)
         N.call("nrms_self_attention", P(self.uqkv), n_clk, None, B, None, B, Nc, wu,
                P(self.uctx), st)
-        rec(6)
+        rec(k + 2)
         N.call("nrms_additive_scores", P(self.uctx), n_clk, wu, P(self.uscores), st)
-        rec(7)
+        rec(k + 3)
         N.call("nrms_additive_pool", P(self.uctx), P(self.uscores), B, Nc, D, P(self.user), st)
-        rec(8)
+        rec(k + 4)
         N.call("nrms_score", P(self.news[n_clk:]), B, C, C * D, D, P(self.user), D, D,
                P(self.logits), st)
-        rec(9)
+        rec(k + 5)
         return self.logits
 
     # Algorithmic work per launch of each stage (SURVEY §8d conventions:
@@ -112,6 +122,11 @@ class ForwardPlan:
                               bytes=n_all * L * (4 * 3 * D + (8 if self.folded else 0) + 4 * D)),
             "addscore_news": dict(flop=2 * n_all * L * D * Q, bytes=4 * (n_all * L * (D + 1) + Q * D)),
             "pool_news": dict(flop=2 * n_all * L * D, bytes=4 * (n_all * L * (D + 1) + n_all * D)),
+            # fused tail: gathered q|k|v rows + ids in, context scratch written once
+            # (re-read from L2 for pooling), news vectors out
+            "news_fused": dict(flop=att_flop(n_all, L) + 2 * n_all * L * D * Q + 2 * n_all * L * D,
+                               bytes=n_all * L * (4 * 3 * D + (8 if self.folded else 0) + 4 * D)
+                               + 4 * (n_all * D + Q * D)),
             "qkv_user": dict(flop=2 * n_clk * D * 3 * D, bytes=4 * (n_clk * 4 * D + 3 * D * D)),
             "mhsa_user": dict(flop=att_flop(B, Nc), bytes=4 * n_clk * 4 * D),
             "addscore_user": dict(flop=2 * n_clk * D * Q, bytes=4 * (n_clk * (D + 1) + Q * D)),

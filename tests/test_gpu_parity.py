@@ -233,6 +233,39 @@ def test_full_vocab_forward_vs_oracle(device):
         assert np.abs(y - ref).max() <= TOL * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 4099])
+def test_fused_news_tail_vs_stages(device, n):
+    """Fused tail == separate stage kernels (within fp32 reordering), including
+    partial last blocks (n % 4 != 0), through both id arrays."""
+    from newsrecommendationsystem_amd import _native as N
+    V = 1000
+    sd = W.nrms_state(21, V)
+    m = _module(sd, V, device, hip_cache_folded_table=False)
+    ne = m.news_encoder
+    qkv = ne.folded_table()
+    ids = torch.from_numpy(W.titles(21, 40 + n, n, V, min_len=1)).to(device)
+    na = n // 2
+    # a NULL first id array means "identity rows" in the ABI, so never pass an empty one
+    ia, ib = (ids[:na].contiguous() if na else ids), ids[na:].contiguous()
+    w, keep = ne.weights()
+    st = N.stream_handle(device)
+    out = torch.empty(n, 300, device=device)
+    nb = N.load().nrms_news_attention_pool_workspace_size(n, 20, 300)
+    ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    N.call("nrms_news_attention_pool", N.ptr(qkv), V, N.ptr(ia), na, N.ptr(ib), n, 20,
+           ctypes.byref(w), N.ptr(out), N.ptr(ws), nb, st)
+    ctx = torch.empty(n * 20, 300, device=device)
+    sc = torch.empty(n * 20, device=device)
+    ref = torch.empty(n, 300, device=device)
+    N.call("nrms_self_attention", N.ptr(qkv), V, N.ptr(ia), na, N.ptr(ib), n, 20, ctypes.byref(w),
+           N.ptr(ctx), st)
+    N.call("nrms_additive_attention", N.ptr(ctx), n, 20, ctypes.byref(w), N.ptr(sc), N.ptr(ref), st)
+    err = ((out - ref).norm(dim=1) / ref.norm(dim=1)).max()
+    assert err < 1e-5, float(err)
+    oracle = O.news_encode(ids.cpu().numpy(), sd, np.float64)
+    assert O.normwise_rel_err(_np(out), oracle).max() < TOL
+
+
 def test_full_size_properties(device):
     """BASELINE config 3 (B = 1024, 1+K = 5, 50 clicked, V = 70,976): size-
     independent properties — folded == direct within fp32 rounding, sharding
@@ -277,8 +310,16 @@ def test_stage_abi_matches_module(golden, golden_state, device):
            N.ptr(ctx), st)
     N.call("nrms_additive_attention", N.ptr(ctx), n, L, ctypes.byref(w), N.ptr(sc), N.ptr(out), st)
     with torch.no_grad():
-        ref = m.get_news_vector({"title": ids.cpu()})
-    assert torch.equal(out, ref)
+        ref = m.get_news_vector({"title": ids.cpu()})   # fused tail kernel
+    assert (out - ref).norm() / ref.norm() < 1e-6
+    # the fused entry point on the same projected rows
+    fused = torch.empty(n, 300, device=device)
+    nb = N.load().nrms_news_attention_pool_workspace_size(n, L, 300)
+    ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    N.call("nrms_news_attention_pool", N.ptr(qkv), n * L, None, n, None, n, L, ctypes.byref(w),
+           N.ptr(fused), N.ptr(ws), nb, st)
+    assert torch.equal(fused, ref)
+    assert O.normwise_rel_err(_np(fused), golden["news_out"]).max() < TOL
     # stage 1 alone against the oracle's projection
     x = golden_state["news_encoder.word_embedding.weight"][golden["news_ids"].astype(np.int64)]
     p = "news_encoder.multihead_self_attention"
@@ -286,3 +327,24 @@ def test_stage_abi_matches_module(golden, golden_state, device):
                                        golden_state[f"{p}.{n_}.bias"], np.float64)
                               for n_ in ("W_Q", "W_K", "W_V")], axis=1)
     assert O.normwise_rel_err(_np(qkv), qkv_ref).max() < 1e-5
+
+
+@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_plan_matches_forward(device, fused, mode):
+    """pipeline.ForwardPlan (stage calls, as timed by bench.py) == nrms_forward."""
+    from newsrecommendationsystem_amd.pipeline import ForwardPlan
+    V = 3000
+    sd = W.nrms_state(8, V)
+    m = _module(sd, V, device)
+    cand, clk, _ = W.impressions(8, 77, 33, V)
+    c, k = torch.from_numpy(cand).to(device), torch.from_numpy(clk).to(device)
+    plan = ForwardPlan(m, 33, 5, 50, 20, proj_mode=mode, fused=fused)
+    with torch.no_grad():
+        y = plan.run(c, k).clone()
+        ref = m.forward_ids(c, k, proj_mode=mode)
+    if fused:
+        assert torch.equal(y, ref)
+    else:
+        assert ((y - ref).norm() / ref.norm()) < 1e-5
+    assert np.abs(_np(y) - O.forward(cand, clk, sd, np.float64)).max() <= TOL * np.abs(_np(y)).max()
