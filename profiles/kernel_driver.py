@@ -1,0 +1,60 @@
+"""Run one bench stage in isolation (for rocprofv3 counter passes).
+
+    python profiles/kernel_driver.py <stage> [--iters 10] [--unfused]
+
+Builds the bench workload (B = 1024 impressions, V = 70,976, folded
+projection), runs the full forward once, then launches only `<stage>`
+`iters` times on the same buffers.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from newsrecommendationsystem_amd import _native as N  # noqa: E402
+from newsrecommendationsystem_amd.pipeline import ForwardPlan  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("stage")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--unfused", action="store_true")
+    a = ap.parse_args()
+    dev = torch.device("cuda:0")
+    model = bench.build_model(dev)
+    cand, clk = bench.synth_impressions(1000, 1024, bench.V_WORDS, dev)
+    plan = ForwardPlan(model, 1024, bench.C, bench.N_CLICKED, bench.L, fused=not a.unfused)
+    with torch.no_grad():
+        plan.run(cand, clk)
+        torch.cuda.synchronize()
+        B, C, Nc, L, D, V = plan.B, plan.C, plan.N, plan.L, plan.D, plan.V
+        n_clk, n_all = B * Nc, B * (C + Nc)
+        st = N.stream_handle(dev)
+        P = N.ptr
+        wn, wu = ctypes.byref(plan.wn), ctypes.byref(plan.wu)
+        calls = {
+            "qkv_news": lambda: N.call("nrms_qkv_project", P(plan.table), V, None, V, wn, P(plan.qkv), st),
+            "news_fused": lambda: N.call("nrms_news_attention_pool", P(plan.qkv), V, P(clk), n_clk, P(cand),
+                                         n_all, L, wn, P(plan.news), P(plan.fws), plan.fws.numel(), st),
+            "mhsa_news": lambda: N.call("nrms_self_attention", P(plan.qkv), V, P(clk), n_clk, P(cand), n_all,
+                                        L, wn, P(plan.ctx), st),
+            "addscore_news": lambda: N.call("nrms_additive_scores", P(plan.ctx), n_all * L, wn, P(plan.scores), st),
+            "qkv_user": lambda: N.call("nrms_qkv_project", P(plan.news), n_clk, None, n_clk, wu, P(plan.uqkv), st),
+            "mhsa_user": lambda: N.call("nrms_self_attention", P(plan.uqkv), n_clk, None, B, None, B, Nc, wu,
+                                        P(plan.uctx), st),
+        }
+        for _ in range(a.iters):
+            calls[a.stage]()
+        torch.cuda.synchronize()
+    print("ok", a.stage, a.iters)
+
+
+if __name__ == "__main__":
+    main()
