@@ -154,6 +154,24 @@ int32_t nrms_score(const float* news, int64_t B, int32_t C, int64_t stride_b,
                    int64_t stride_c, const float* user, int64_t stride_u, int32_t D,
                    float* out, hipStream_t stream);
 
+/* Eval-semantics scoring (src/evaluate.py:245-260): out[k] = <news[news_idx[k]],
+ * user[user_idx[k]]> for k < n_pairs — all candidates of all impressions of a
+ * split in one launch (each impression's get_prediction, __init__.py:73-84,
+ * becomes a contiguous run of pairs). Indices out of range give NaN. */
+int32_t nrms_score_pairs(const float* news, int64_t n_news, const float* user, int64_t n_users,
+                         const int64_t* news_idx, const int64_t* user_idx, int64_t n_pairs,
+                         int32_t D, float* out, hipStream_t stream);
+
+/* Per-impression ranking metrics (src/evaluate.py:24-42,160-168) over ragged
+ * impressions: impression i owns scores/labels [offsets[i], offsets[i+1]).
+ * out[i*4 + {0,1,2,3}] = AUC, MRR, nDCG@5, nDCG@10 in fp64; all four NaN when
+ * the impression has one class only or a NaN score (the reference's
+ * ValueError branch). Ranking order = np.argsort(score)[::-1]: descending,
+ * equal scores by larger index first. */
+int32_t nrms_impression_metrics(const float* scores, const int32_t* labels,
+                                const int64_t* offsets, int64_t n_imp, double* out,
+                                hipStream_t stream);
+
 /* NRMS.forward (src/model/NRMS/__init__.py:19-48), eval mode:
  * cand_ids[B, C, L], clicked_ids[B, N, L] -> logits[B, C]. All B*(C+N) titles
  * are encoded (forward semantics), then the user vector and the scores. */

@@ -51,6 +51,8 @@ SIGNATURES = {
     "nrms_user_encode_workspace_size": (_sz, [_i64, _i32, _i32]),
     "nrms_user_encode": (_i32, [_p, _i64, _i32, _EW, _p, _p, _sz, _p]),
     "nrms_score": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p]),
+    "nrms_score_pairs": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _i32, _p, _p]),
+    "nrms_impression_metrics": (_i32, [_p, _p, _p, _i64, _p, _p]),
     "nrms_forward_workspace_size": (_sz, [_i64, _i32, _i32, _i32, _i64, _i32, _i32]),
     "nrms_forward": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _p, _i64, _EW, _EW, _i32, _p, _p,
                             _sz, _p]),

@@ -286,6 +286,22 @@ int32_t nrms_score(const float* news, int64_t B, int32_t C, int64_t stride_b, in
   return launch_score(news, B, C, stride_b, stride_c, user, stride_u, D, out, stream);
 }
 
+int32_t nrms_score_pairs(const float* news, int64_t n_news, const float* user, int64_t n_users,
+                         const int64_t* news_idx, const int64_t* user_idx, int64_t n_pairs,
+                         int32_t D, float* out, hipStream_t stream) {
+  if (n_pairs < 0 || n_news < 0 || n_users < 0 || D <= 0) return NRMS_ERR_INVALID_ARG;
+  if (n_pairs > 0 && (!news || !user || !news_idx || !user_idx || !out)) return NRMS_ERR_INVALID_ARG;
+  return launch_score_pairs(news, n_news, user, n_users, news_idx, user_idx, n_pairs, D, out, stream);
+}
+
+int32_t nrms_impression_metrics(const float* scores, const int32_t* labels,
+                                const int64_t* offsets, int64_t n_imp, double* out,
+                                hipStream_t stream) {
+  if (n_imp < 0) return NRMS_ERR_INVALID_ARG;
+  if (n_imp > 0 && (!scores || !labels || !offsets || !out)) return NRMS_ERR_INVALID_ARG;
+  return launch_impression_metrics(scores, labels, offsets, n_imp, out, stream);
+}
+
 size_t nrms_forward_workspace_size(int64_t B, int32_t C, int32_t N, int32_t L, int64_t V,
                                    int32_t D, int32_t proj_mode) {
   if (B < 0 || C < 0 || N <= 0 || L <= 0 || V < 0 || D <= 0) return 0;

@@ -85,6 +85,12 @@ int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a
                           const int64_t* ids_b, int64_t n_titles, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* ctx,
                           float* out, hipStream_t s);
+int32_t launch_score_pairs(const float* news, int64_t n_news, const float* user, int64_t n_users,
+                           const int64_t* news_idx, const int64_t* user_idx, int64_t n_pairs,
+                           int D, float* out, hipStream_t s);
+int32_t launch_impression_metrics(const float* scores, const int32_t* labels,
+                                  const int64_t* offsets, int64_t n_imp, double* out,
+                                  hipStream_t s);
 int32_t launch_score(const float* news, int64_t B, int C, int64_t sb, int64_t sc,
                      const float* user, int64_t su, int D, float* out, hipStream_t s);
 

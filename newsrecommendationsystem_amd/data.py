@@ -1,0 +1,184 @@
+"""On-disk formats of the reference and a synthetic MIND-shaped generator.
+
+Readers (host side, build the id arrays the HIP path consumes):
+  * news_parsed.tsv   id, category, subcategory, title, abstract, title_entities,
+                      abstract_entities — title is a python list literal of
+                      num_words_title ints (src/data_preprocess.py:115-139,205,239;
+                      read by src/evaluate.py:55-71, src/dataset.py:28-43)
+  * behaviors.tsv     raw MIND rows without header: impression_id, user, time,
+                      clicked_news (space separated), impressions ("N1-1 N2-0 ...")
+                      (src/evaluate.py:133-157)
+  * behaviors_parsed.tsv  user, clicked_news, candidate_news, clicked (train
+                      split, src/data_preprocess.py:71-81; src/dataset.py:64-85)
+  * pretrained_word_embedding.npy  float [V, 300] (src/data_preprocess.py:280,
+                      loaded at src/train.py:76-80)
+
+Writers produce the same formats for the synthetic generator (MIND data and
+GloVe are not available offline).
+"""
+import ast
+import csv
+import os
+
+import numpy as np
+
+NUM_WORDS_TITLE = 20
+NUM_CLICKED = 50
+PADDED_NEWS = "PADDED_NEWS"
+
+
+# ---------------------------------------------------------------- readers
+class NewsCorpus:
+    """news_parsed.tsv: ids (str), titles int64 [n, L]; id -> first row (the
+    reference keeps the first vector per id, src/evaluate.py:197-201)."""
+
+    def __init__(self, ids, titles):
+        self.ids = list(ids)
+        self.titles = np.ascontiguousarray(titles, dtype=np.int64)
+        self.index = {}
+        for i, nid in enumerate(self.ids):
+            self.index.setdefault(nid, i)
+
+    def __len__(self):
+        return len(self.ids)
+
+
+def read_news_parsed(path, num_words_title=NUM_WORDS_TITLE):
+    ids, titles = [], []
+    with open(path, newline="") as f:
+        rd = csv.reader(f, delimiter="\t", quoting=csv.QUOTE_NONE)
+        header = next(rd)
+        ci, ct = header.index("id"), header.index("title")
+        for row in rd:
+            ids.append(row[ci])
+            t = ast.literal_eval(row[ct])
+            if len(t) != num_words_title:
+                raise ValueError(f"title of {row[ci]} has {len(t)} ids, expected {num_words_title}")
+            titles.append(t)
+    return NewsCorpus(ids, np.array(titles, dtype=np.int64).reshape(-1, num_words_title))
+
+
+class Impression:
+    __slots__ = ("impression_id", "user", "time", "clicked_news", "candidates", "labels")
+
+    def __init__(self, impression_id, user, time, clicked_news, candidates, labels):
+        self.impression_id = impression_id
+        self.user = user
+        self.time = time
+        self.clicked_news = clicked_news      # the raw history string (user-cache key)
+        self.candidates = candidates          # list of news ids
+        self.labels = labels                  # list of int
+
+
+def read_behaviors(path):
+    """Raw behaviors.tsv (header=None). An empty history becomes ' ' like the
+    reference's fillna(' ') (src/evaluate.py:91,142)."""
+    out = []
+    with open(path, newline="") as f:
+        for line in f:
+            line = line.rstrip("\n")
+            if not line:
+                continue
+            cols = line.split("\t")
+            cols += [""] * (5 - len(cols))
+            hist = cols[3] if cols[3] != "" else " "
+            cands, labels = [], []
+            for tok in cols[4].split():
+                nid, lab = tok.split("-")[0], tok.split("-")[1]
+                cands.append(nid)
+                labels.append(int(lab))
+            out.append(Impression(cols[0], cols[1], cols[2], hist, cands, labels))
+    return out
+
+
+def history_ids(history_string, num_clicked=NUM_CLICKED):
+    """First num_clicked ids of the history, left-padded with PADDED_NEWS
+    (src/evaluate.py:115-124)."""
+    h = history_string.split()[:num_clicked]
+    return [PADDED_NEWS] * (num_clicked - len(h)) + h
+
+
+def read_behaviors_parsed(path, corpus, num_clicked=NUM_CLICKED):
+    """Train-split rows -> (candidates [n, 1+K, L], clicked [n, N, L], clicked
+    labels [n, 1+K]): the batch contract of BaseDataset.__getitem__
+    (src/dataset.py:64-85): history truncated to its first N, left-padded with
+    all-zero titles."""
+    L = corpus.titles.shape[1]
+    cands, clks, labs = [], [], []
+    with open(path, newline="") as f:
+        rd = csv.reader(f, delimiter="\t", quoting=csv.QUOTE_NONE)
+        header = next(rd)
+        cc, cn, cl = (header.index(x) for x in ("clicked_news", "candidate_news", "clicked"))
+        for row in rd:
+            cand = [corpus.titles[corpus.index[x]] for x in row[cn].split()]
+            hist = [corpus.titles[corpus.index[x]] for x in row[cc].split()[:num_clicked]]
+            pad = [np.zeros(L, np.int64)] * (num_clicked - len(hist))
+            cands.append(np.stack(cand))
+            clks.append(np.stack(pad + hist) if pad + hist else np.zeros((num_clicked, L), np.int64))
+            labs.append([int(x) for x in row[cl].split()])
+    return np.stack(cands), np.stack(clks), np.array(labs, dtype=np.int64)
+
+
+# ---------------------------------------------------------------- writers
+def write_news_parsed(path, ids, titles):
+    with open(path, "w", newline="") as f:
+        w = csv.writer(f, delimiter="\t", quoting=csv.QUOTE_NONE, escapechar="\\", lineterminator="\n")
+        w.writerow(["id", "category", "subcategory", "title", "abstract", "title_entities",
+                    "abstract_entities"])
+        zero_a = str([0] * 50)
+        for nid, t in zip(ids, titles):
+            w.writerow([nid, 0, 0, "[" + ", ".join(str(int(x)) for x in t) + "]", zero_a,
+                        str([0] * len(t)), zero_a])
+
+
+def write_behaviors(path, impressions):
+    with open(path, "w") as f:
+        for im in impressions:
+            hist = "" if im.clicked_news.strip() == "" else im.clicked_news
+            imps = " ".join(f"{c}-{l}" for c, l in zip(im.candidates, im.labels))
+            f.write(f"{im.impression_id}\t{im.user}\t{im.time}\t{hist}\t{imps}\n")
+
+
+# ---------------------------------------------------------------- synthetic MIND-shaped split
+def synthetic_split(directory, seed=0, n_news=4000, n_users=600, n_impressions=2000, V=70976,
+                    min_cands=2, max_cands=40, teacher=None, temperature=1.0):
+    """Write news_parsed.tsv + behaviors.tsv under `directory`.
+
+    Titles: length U{5..20} right-padded with 0, ids U[1, V). Users: history of
+    U{0..70} clicked news (so some exceed the 50-item truncation and some are
+    empty). Impressions: U{min_cands..max_cands} distinct candidates; labels are
+    drawn from a planted teacher when `teacher(corpus, impressions) -> [logits]`
+    is given (y ~ Bernoulli(sigmoid(logit / temperature)), so AUC is
+    informative), otherwise uniformly with p = 0.2. Returns (corpus, impressions).
+    """
+    rng = np.random.default_rng(seed)
+    os.makedirs(directory, exist_ok=True)
+    L = NUM_WORDS_TITLE
+    ids = [f"N{i}" for i in range(n_news)]
+    lens = rng.integers(5, L + 1, n_news)
+    titles = rng.integers(1, V, (n_news, L))
+    titles[np.arange(L)[None, :] >= lens[:, None]] = 0
+    users = []
+    for u in range(n_users):
+        h = rng.integers(0, 71)
+        users.append(" ".join(f"N{x}" for x in rng.integers(0, n_news, h)))
+    imps = []
+    for k in range(n_impressions):
+        u = int(rng.integers(0, n_users))
+        c = int(rng.integers(min_cands, max_cands + 1))
+        # distinct candidates per impression, as in MIND (no exact score ties)
+        cand = [f"N{x}" for x in rng.choice(n_news, size=min(c, n_news), replace=False)]
+        imps.append(Impression(str(k + 1), f"U{u}", "11/15/2019 10:00:00 AM", users[u] or " ", cand,
+                               [0] * c))
+    if teacher is not None:
+        corpus = NewsCorpus(ids, titles)
+        logits = teacher(corpus, imps)
+        for im, lg in zip(imps, logits):
+            p = 1.0 / (1.0 + np.exp(-np.asarray(lg, np.float64) / temperature))
+            im.labels = [int(x) for x in (rng.random(len(p)) < p)]
+    else:
+        for im in imps:
+            im.labels = [int(x) for x in (rng.random(len(im.candidates)) < 0.2)]
+    write_news_parsed(os.path.join(directory, "news_parsed.tsv"), ids, titles)
+    write_behaviors(os.path.join(directory, "behaviors.tsv"), imps)
+    return NewsCorpus(ids, titles), imps

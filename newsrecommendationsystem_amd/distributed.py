@@ -1,0 +1,61 @@
+"""Multi-GPU layout of the scoring path: one process per GPU,
+weights replicated, impressions sharded by user so a user's history lives on
+one rank; no collective on the data path. The only collective is the final
+reduction of the per-impression metric sums (5 fp64 words per rank), over
+RCCL (backend "nccl" on ROCm) between GPUs or gloo on CPU.
+
+The reference has no distributed code (SURVEY §0 finding 1); this module is
+new, and tests/test_distributed_cpu.py covers it with world_size 2 on gloo.
+"""
+import os
+import zlib
+
+import torch
+
+
+def user_rank(user, world):
+    """Stable owner rank of a user id (Python's hash() is salted per process)."""
+    return zlib.crc32(str(user).encode()) % world
+
+
+def shard_impressions(impressions, rank, world):
+    """The impressions whose user this rank owns, in their original order."""
+    if world <= 1:
+        return list(impressions)
+    return [im for im in impressions if user_rank(im.user, world) == rank]
+
+
+def shard_rows(n, rank, world):
+    """Contiguous [start, stop) slice of n independent units for weak/strong
+    scaling of synthetic batches."""
+    per = (n + world - 1) // world
+    return min(n, rank * per), min(n, (rank + 1) * per)
+
+
+def all_reduce_sums(sums, counts, group=None):
+    """Sum (metric_sum[4], count[4]) over ranks in one collective."""
+    import torch.distributed as dist
+    buf = torch.cat([sums.to(torch.float64), counts.to(torch.float64)])
+    if dist.get_backend(group) == "gloo" and buf.is_cuda:
+        host = buf.cpu()
+        dist.all_reduce(host, group=group)
+        buf = host.to(buf.device)
+    else:
+        dist.all_reduce(buf, group=group)
+    return buf[:4], buf[4:]
+
+
+def init_from_env(backend=None):
+    """torch.distributed.run environment -> (rank, world, local_rank, initialised?)."""
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        kw = {}
+        if backend == "nccl":
+            kw["device_id"] = torch.device("cuda", local)
+        dist.init_process_group(backend, **kw)
+    return rank, world, local, world > 1

@@ -1,0 +1,168 @@
+"""Eval-semantics scoring pipeline on the HIP path (drop-in for
+src/evaluate.py:171-272).
+
+The reference scores a split in three host-driven passes: news vectors cached
+in a dict, user vectors cached per history string, then a Python loop with
+batch size 1 over impressions (one get_prediction and one device->host sync
+each), and finally per-impression AUC/MRR/nDCG in a process pool. Here every
+pass is one (or a few) launches over flat index arrays built once on the
+host:
+
+  1. news vectors of the whole corpus: NRMS.get_news_vector (HIP NewsEncoder),
+     plus one all-zero row for PADDED_NEWS (evaluate.py:203-204);
+  2. user vectors of every distinct history string: the clicked-news rows are
+     gathered from the news-vector table by nrms_embedding_gather and encoded
+     by NRMS.get_user_vector (HIP UserEncoder);
+  3. all impressions' candidate logits in one nrms_score_pairs launch;
+  4. per-impression metrics in one nrms_impression_metrics launch, then the
+     nanmean (evaluate.py:270-272) — or, across ranks, an all-reduce of
+     (sum, count) per metric.
+"""
+import sys
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .data import PADDED_NEWS, history_ids, read_behaviors, read_news_parsed
+
+
+class EvalPlan:
+    """Host-side index arrays for one split (built once, reused per model)."""
+
+    def __init__(self, corpus, impressions, max_count=sys.maxsize, num_clicked=50):
+        # the reference breaks when count == max_count before scoring it
+        # (src/evaluate.py:245-249): impressions 1..max_count-1 are scored
+        n = len(impressions) if max_count > len(impressions) else max(0, max_count - 1)
+        self.impressions = impressions[:n]
+        self.corpus = corpus
+        pad = len(corpus)
+        hist_of = {}
+        hists = []
+        pair_user, cand, labels, offsets = [], [], [], [0]
+        for im in self.impressions:
+            u = hist_of.get(im.clicked_news)
+            if u is None:
+                u = hist_of[im.clicked_news] = len(hists)
+                hists.append(im.clicked_news)
+            for c, y in zip(im.candidates, im.labels):
+                cand.append(corpus.index[c])          # KeyError like news2vector[...]
+                labels.append(y)
+                pair_user.append(u)
+            offsets.append(len(cand))
+        self.hist_rows = np.array(
+            [[pad if x == PADDED_NEWS else corpus.index[x] for x in history_ids(h, num_clicked)]
+             for h in hists], dtype=np.int64).reshape(len(hists), num_clicked)
+        self.cand = np.array(cand, dtype=np.int64)
+        self.pair_user = np.array(pair_user, dtype=np.int64)
+        self.labels = np.array(labels, dtype=np.int32)
+        self.offsets = np.array(offsets, dtype=np.int64)
+        self.num_clicked = num_clicked
+
+    @property
+    def n_impressions(self):
+        return len(self.offsets) - 1
+
+
+@torch.no_grad()
+def news_vectors(model, titles, chunk=65536):
+    """[n + 1, D] news-vector table on the model's device; last row = PADDED_NEWS."""
+    ne = model.news_encoder
+    dev = ne.word_embedding.weight.device
+    D = ne.word_embedding.embedding_dim
+    n = titles.shape[0]
+    out = torch.zeros(n + 1, D, dtype=torch.float32, device=dev)
+    t = torch.from_numpy(titles) if isinstance(titles, np.ndarray) else titles
+    for a in range(0, n, chunk):
+        b = min(n, a + chunk)
+        out[a:b] = model.get_news_vector({"title": t[a:b]})
+    return out
+
+
+@torch.no_grad()
+def user_vectors(model, news_tab, hist_rows, chunk=16384):
+    """User vectors of every history: gather clicked rows (PADDED -> zero row)
+    then the HIP UserEncoder."""
+    dev = news_tab.device
+    U, Nc = hist_rows.shape
+    D = news_tab.shape[1]
+    out = torch.empty(U, D, dtype=torch.float32, device=dev)
+    rows = torch.from_numpy(hist_rows).to(dev)
+    for a in range(0, U, chunk):
+        r = rows[a:a + chunk].contiguous()
+        b = r.shape[0]
+        x = torch.empty(b * Nc, D, dtype=torch.float32, device=dev)
+        N.call("nrms_embedding_gather", N.ptr(r), b * Nc, N.ptr(news_tab), news_tab.shape[0], D,
+               N.ptr(x), N.stream_handle(dev))
+        out[a:a + b] = model.get_user_vector(x.view(b, Nc, D))
+    return out
+
+
+@torch.no_grad()
+def score_plan(model, plan):
+    """Logits of every (impression, candidate) pair and the per-impression
+    metric table [n_imp, 4] (AUC, MRR, nDCG@5, nDCG@10; fp64) on the device."""
+    news_tab = news_vectors(model, plan.corpus.titles)
+    dev = news_tab.device
+    D = news_tab.shape[1]
+    users = user_vectors(model, news_tab, plan.hist_rows)
+    K = plan.cand.shape[0]
+    scores = torch.empty(K, dtype=torch.float32, device=dev)
+    cand = torch.from_numpy(plan.cand).to(dev)
+    pu = torch.from_numpy(plan.pair_user).to(dev)
+    st = N.stream_handle(dev)
+    N.call("nrms_score_pairs", N.ptr(news_tab), news_tab.shape[0], N.ptr(users), users.shape[0],
+           N.ptr(cand), N.ptr(pu), K, D, N.ptr(scores), st)
+    labels = torch.from_numpy(plan.labels).to(dev)
+    offsets = torch.from_numpy(plan.offsets).to(dev)
+    metrics = torch.empty(plan.n_impressions, 4, dtype=torch.float64, device=dev)
+    N.call("nrms_impression_metrics", N.ptr(scores), N.ptr(labels), N.ptr(offsets),
+           plan.n_impressions, N.ptr(metrics), st)
+    return scores, metrics
+
+
+def nan_sums(metrics):
+    """(sum, count) per metric column over non-NaN rows (fp64)."""
+    ok = ~torch.isnan(metrics)
+    return torch.where(ok, metrics, torch.zeros_like(metrics)).sum(0), ok.sum(0).to(torch.float64)
+
+
+def reduce_means(sums, counts):
+    with np.errstate(invalid="ignore"):
+        return tuple(float(x) for x in (sums / counts).cpu().numpy())
+
+
+@torch.no_grad()
+def evaluate(model, directory, num_workers=4, max_count=sys.maxsize, process_group=None):
+    """Same signature and return value as the reference's evaluate()
+    (src/evaluate.py:171-184): (AUC, MRR, nDCG@5, nDCG@10) of the split in
+    `directory` (news_parsed.tsv + behaviors.tsv). `num_workers` is accepted
+    for compatibility (there is no process pool). With a torch.distributed
+    `process_group`, each rank scores the impressions of its users
+    (zlib.crc32(user) % world) and the metric sums are all-reduced."""
+    import os
+    corpus = read_news_parsed(os.path.join(directory, "news_parsed.tsv"))
+    imps = read_behaviors(os.path.join(directory, "behaviors.tsv"))
+    return evaluate_split(model, corpus, imps, max_count, process_group)
+
+
+@torch.no_grad()
+def evaluate_split(model, corpus, impressions, max_count=sys.maxsize, process_group=None):
+    n = len(impressions) if max_count > len(impressions) else max(0, max_count - 1)
+    imps = impressions[:n]
+    if process_group is not None:
+        from .distributed import shard_impressions
+        import torch.distributed as dist
+        imps = shard_impressions(imps, dist.get_rank(process_group), dist.get_world_size(process_group))
+    plan = EvalPlan(corpus, imps, num_clicked=model.config.num_clicked_news_a_user)
+    if plan.n_impressions:
+        _, metrics = score_plan(model, plan)
+        sums, counts = nan_sums(metrics)
+    else:
+        dev = model.news_encoder.word_embedding.weight.device
+        sums = torch.zeros(4, dtype=torch.float64, device=dev)
+        counts = torch.zeros(4, dtype=torch.float64, device=dev)
+    if process_group is not None:
+        from .distributed import all_reduce_sums
+        sums, counts = all_reduce_sums(sums, counts, process_group)
+    return reduce_means(sums, counts)
