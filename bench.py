@@ -99,6 +99,43 @@ def cpu_baseline(model, device, sample_B=32, min_seconds=12.0, max_reps=500):
     return info, parity
 
 
+def eval_auc_check(model, device, n_impressions=4000, seed=11):
+    """The metric's second half, "AUC vs CPU ref": a synthetic MIND-shaped split
+    (reference file formats) whose labels are drawn from this model's own
+    logits (planted teacher, temperature 1), scored by the GPU eval pipeline
+    (newsrecommendationsystem_amd.evaluate) and by the CPU restatement of
+    src/evaluate.py (oracle/eval_oracle.py, the cpu_baseline leg)."""
+    import tempfile
+    import numpy as np
+    from newsrecommendationsystem_amd import data as Dt
+    from newsrecommendationsystem_amd.evaluate import EvalPlan, evaluate, score_plan
+    from oracle import eval_oracle as EO
+
+    def teacher(corpus, imps):
+        scores, _ = score_plan(model, EvalPlan(corpus, imps))
+        sc = scores.cpu().numpy()
+        plan = EvalPlan(corpus, imps)
+        return [sc[a:b] for a, b in zip(plan.offsets[:-1], plan.offsets[1:])]
+
+    with tempfile.TemporaryDirectory() as d:
+        corpus, imps = Dt.synthetic_split(d, seed=seed, n_news=6000, n_users=1500,
+                                          n_impressions=n_impressions, V=V_WORDS, teacher=teacher)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        gpu = evaluate(model, d)
+        torch.cuda.synchronize()
+        t_gpu = time.perf_counter() - t0
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    t0 = time.perf_counter()
+    cpu, _, _ = EO.evaluate(sd, corpus, imps)
+    t_cpu = time.perf_counter() - t0
+    return {"impressions": n_impressions, "auc_gpu": gpu[0], "auc_cpu": cpu[0],
+            "abs_diff_auc": abs(gpu[0] - cpu[0]), "tolerance": 0.002,
+            "mrr_gpu": gpu[1], "mrr_cpu": cpu[1], "ndcg10_gpu": gpu[3], "ndcg10_cpu": cpu[3],
+            "eval_wall_s_gpu_incl_file_io": round(t_gpu, 3), "eval_wall_s_cpu": round(t_cpu, 3),
+            "labels": "planted teacher (Bernoulli(sigmoid(model logit)))"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -197,6 +234,7 @@ def main():
         cb, parity = cpu_baseline(model, device)
         out["cpu_baseline"] = cb
         out["parity_vs_cpu"] = parity
+        out["auc_vs_cpu"] = eval_auc_check(model, device)
     else:
         out["cpu_baseline"] = None
     if rank == 0:
