@@ -9,7 +9,7 @@
 // gfx950 specifics: v_mfma_f32_16x16x4_f32 (exact fp32, 256 FLOP/clk/CU);
 // 4 waves x (32 rows x 16·TN cols) per 128-row block; K staged through LDS in
 // 32-deep chunks with register prefetch of the next chunk; each lane reads
-// its A/B fragments with conflict-free ds_read_b64 (row stride 36 floats);
+// its A/B fragments with conflict-free ds_read_b128 (row stride 40 floats);
 // XCD-aware block order so the column tiles of one row tile share an L2.
 #include "nrms_common.hpp"
 
@@ -18,12 +18,12 @@ namespace {
 
 constexpr int BM = 128;
 constexpr int BK = 32;
-constexpr int LDS_LD = 36;  // floats; ≡ 4 (mod 64)/..: b64 fragment reads are conflict-free
+constexpr int LDS_LD = 40;  // floats: ds_read_b128 fragment reads conflict-free, rows 16-B aligned
 constexpr int kThreads = 256;
 
-// K-permutation: MFMA step (p, t) gives lane group kq (= lane >> 4) the K index
-// 8p + 2kq + t, so each lane fetches its two consecutive K values with one
-// ds_read_b64; A and B use the same map, so every K term is summed once.
+// K-permutation: MFMA step (c, t) gives lane group kq (= lane >> 4) the K index
+// 16c + 4kq + t, so each lane fetches its four consecutive K values with one
+// ds_read_b128; A and B use the same map, so every K term is summed once.
 template <int TN, bool ADDITIVE>
 __global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
     const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
@@ -99,8 +99,8 @@ __global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
     for (int tn = 0; tn < TN; ++tn) acc[ms][tn] = floatx4{0.f, 0.f, 0.f, 0.f};
 
   const int lm = lane & 15, kq = lane >> 4;
-  const float* Aw = As + (wave * 32 + lm) * LDS_LD + 2 * kq;
-  const float* Bw = Bs + lm * LDS_LD + 2 * kq;
+  const float* Aw = As + (wave * 32 + lm) * LDS_LD + 4 * kq;
+  const float* Bw = Bs + lm * LDS_LD + 4 * kq;
 
   const int nk = (K + BK - 1) / BK;
   gload(0);
@@ -109,22 +109,30 @@ __global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
   for (int kc = 0; kc < nk; ++kc) {
     if (kc + 1 < nk) gload(kc + 1);
 #pragma unroll
-    for (int p = 0; p < BK / 8; ++p) {
-      const float2 a0 = *reinterpret_cast<const float2*>(Aw + 8 * p);
-      const float2 a1 = *reinterpret_cast<const float2*>(Aw + 16 * LDS_LD + 8 * p);
-      float2 b[TN];
+    for (int c = 0; c < BK / 16; ++c) {
+      const float4 a0 = *reinterpret_cast<const float4*>(Aw + 16 * c);
+      const float4 a1 = *reinterpret_cast<const float4*>(Aw + 16 * LDS_LD + 16 * c);
+      // B fragments two column tiles at a time: 4 independent accumulators per
+      // k-step keep the MFMA pipe busy without holding all TN fragments live.
 #pragma unroll
-      for (int tn = 0; tn < TN; ++tn)
-        b[tn] = *reinterpret_cast<const float2*>(Bw + tn * 16 * LDS_LD + 8 * p);
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        acc[0][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b[tn].x, acc[0][tn], 0, 0, 0);
-        acc[1][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b[tn].x, acc[1][tn], 0, 0, 0);
-      }
-#pragma unroll
-      for (int tn = 0; tn < TN; ++tn) {
-        acc[0][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b[tn].y, acc[0][tn], 0, 0, 0);
-        acc[1][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b[tn].y, acc[1][tn], 0, 0, 0);
+      for (int tn = 0; tn < TN; tn += 2) {
+        const float4 b0 = *reinterpret_cast<const float4*>(Bw + tn * 16 * LDS_LD + 16 * c);
+        if (tn + 1 < TN) {
+          const float4 b1 = *reinterpret_cast<const float4*>(Bw + (tn + 1) * 16 * LDS_LD + 16 * c);
+#define NRMS_MFMA4(F)                                                                             \
+  acc[0][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.F, b0.F, acc[0][tn], 0, 0, 0);             \
+  acc[1][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.F, b0.F, acc[1][tn], 0, 0, 0);             \
+  acc[0][tn + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.F, b1.F, acc[0][tn + 1], 0, 0, 0);     \
+  acc[1][tn + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.F, b1.F, acc[1][tn + 1], 0, 0, 0);
+          NRMS_MFMA4(x) NRMS_MFMA4(y) NRMS_MFMA4(z) NRMS_MFMA4(w)
+#undef NRMS_MFMA4
+        } else {
+#define NRMS_MFMA2(F)                                                                             \
+  acc[0][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.F, b0.F, acc[0][tn], 0, 0, 0);             \
+  acc[1][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.F, b0.F, acc[1][tn], 0, 0, 0);
+          NRMS_MFMA2(x) NRMS_MFMA2(y) NRMS_MFMA2(z) NRMS_MFMA2(w)
+#undef NRMS_MFMA2
+        }
       }
     }
     __syncthreads();
