@@ -14,13 +14,16 @@ eager fallback: without the built library every call raises.
 Differences from the reference that a caller can observe:
   * the device is the module's own device (``.to(device)``), not a global
     ``cuda:0`` (src/model/NRMS/news_encoder.py:7), so one process per GPU works;
-  * eval mode only in this ABI version: training mode raises (dropout and the
-    backward kernels are not built yet).
+  * training mode (``model.train()``) runs the reference's op sequence with
+    dropout on ATen autograd (newsrecommendationsystem_amd/train.py) so
+    src/train.py can drive this module; the HIP kernels are the eval-mode
+    scoring path (the north-star path) and the HIP backward is not built yet.
 """
 import torch
 import torch.nn as nn
 
 from . import _native as N
+from . import train as _train
 from .config import NRMSConfig
 
 
@@ -138,7 +141,8 @@ class NewsEncoder(nn.Module):
 
     # -- reference interface --------------------------------------------------
     def forward(self, news):
-        _eval_only(self)
+        if self.training:
+            return _train.news_encode_autograd(self, self._ids(news["title"]))
         ids = self._ids(news["title"])
         n, L = ids.shape
         tab = self.table()
@@ -179,7 +183,9 @@ class UserEncoder(nn.Module):
         return _encoder_struct(self.multihead_self_attention, self.additive_attention)
 
     def forward(self, user_vector):
-        _eval_only(self)
+        if self.training:
+            dev = self.additive_attention.attention_query_vector.device
+            return _train.user_encode_autograd(self, user_vector.to(dev))
         dev = self.additive_attention.attention_query_vector.device
         x = _f32(user_vector.to(dev))
         B, n_clicked, D = x.shape
@@ -198,6 +204,8 @@ class DotProductClickPredictor(nn.Module):
     """src/model/general/click_predictor/dot_product.py:4-19 on the HIP path."""
 
     def forward(self, candidate_news_vector, user_vector):
+        if self.training:  # differentiable (dot_product.py:10-19)
+            return torch.bmm(candidate_news_vector, user_vector.unsqueeze(dim=2)).squeeze(dim=2)
         news = _f32(candidate_news_vector)
         user = _f32(user_vector.to(news.device))
         B, C, D = news.shape
@@ -223,16 +231,17 @@ class NRMS(nn.Module):
     def forward(self, candidate_news, clicked_news):
         """candidate_news: list (1+K) of {"title": LongTensor[B, L]};
         clicked_news: list (N) of the same -> logits [B, 1+K]. One fused
-        launch sequence for all B*(1+K+N) titles (src/model/NRMS/__init__.py:19-48)."""
-        _eval_only(self)
+        launch sequence for all B*(1+K+N) titles (src/model/NRMS/__init__.py:19-48).
+        In training mode: the autograd path of train.py, dropout included."""
         cand = torch.stack([x["title"] for x in candidate_news], dim=1)
         clk = torch.stack([x["title"] for x in clicked_news], dim=1)
         return self.forward_ids(cand, clk)
 
     def forward_ids(self, cand_ids, clicked_ids, proj_mode=None):
         """Tensor form of forward: cand_ids [B, C, L], clicked_ids [B, N, L]."""
-        _eval_only(self)
         ne = self.news_encoder
+        if self.training:
+            return _train.forward_autograd(self, ne._ids(cand_ids), ne._ids(clicked_ids))
         cand = ne._ids(cand_ids)
         clk = ne._ids(clicked_ids)
         B, C, L = cand.shape
@@ -261,13 +270,6 @@ class NRMS(nn.Module):
     def get_prediction(self, news_vector, user_vector):
         return self.click_predictor(news_vector.unsqueeze(dim=0),
                                     user_vector.unsqueeze(dim=0)).squeeze(dim=0)
-
-
-def _eval_only(module):
-    if module.training:
-        raise NotImplementedError(
-            "newsrecommendationsystem_amd NRMS: ABI v1 implements eval-mode scoring only "
-            "(dropout + backward kernels are not built yet); call model.eval()")
 
 
 def ctypes_byref(s):

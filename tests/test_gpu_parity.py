@@ -178,13 +178,17 @@ def test_out_of_range_ids_raise(gold_model, golden):
         gold_model.get_news_vector({"title": torch.tensor([[-1, 3]])})
 
 
-def test_training_mode_raises(gold_model):
-    gold_model.train()
-    try:
-        with pytest.raises(NotImplementedError):
-            gold_model.get_news_vector({"title": torch.zeros(2, 20, dtype=torch.long)})
-    finally:
-        gold_model.eval()
+def test_train_mode_forward_matches_hip_eval(golden, golden_state, device):
+    """Training mode (ATen autograd, dropout p=0) and the HIP eval path agree."""
+    V = int(golden["V"])
+    m = _module(golden_state, V, device, dropout_probability=0.0)
+    cand = torch.from_numpy(golden["fwd_cand"].astype(np.int64))
+    clk = torch.from_numpy(golden["fwd_clicked"].astype(np.int64))
+    ev = _np(m.forward_ids(cand, clk))
+    m.train()
+    tr = m.forward_ids(cand, clk)
+    assert tr.requires_grad
+    assert np.abs(_np(tr) - ev).max() / np.abs(ev).max() < 1e-5
 
 
 @pytest.mark.parametrize("L", [1, 5, 20, 32, 50, 64])
