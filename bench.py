@@ -136,6 +136,63 @@ def eval_auc_check(model, device, n_impressions=4000, seed=11):
             "labels": "planted teacher (Bernoulli(sigmoid(model logit)))"}
 
 
+def _time_launches(fn, reps, device):
+    """Average ms of fn() over reps launches, HIP events on the launch stream."""
+    s = torch.cuda.current_stream(device)
+    fn()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(s)
+    for _ in range(reps):
+        fn()
+    e1.record(s)
+    e1.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def gather_hbm(device, V=1 << 20, n_titles=100_000, reps=20):
+    """SURVEY §8d gather figure: nrms_embedding_gather alone over a 1.26 GB
+    table (V = 1,048,576, beyond the 256 MB Infinity Cache), config-2 shape
+    (100k titles x 20 tokens). Algorithmic bytes per token: 8 (id) + 1200
+    (row read) + 1200 (row write)."""
+    from newsrecommendationsystem_amd import _native as Nat
+    gen = torch.Generator(device=device).manual_seed(5)
+    table = torch.randn(V, D, generator=gen, device=device)
+    ids = synth_titles(gen, n_titles, V, device).reshape(-1).contiguous()
+    out = torch.empty(ids.numel(), D, device=device)
+    st = Nat.stream_handle(device)
+    fn = lambda: Nat.call("nrms_embedding_gather", Nat.ptr(ids), ids.numel(), Nat.ptr(table), V, D,
+                          Nat.ptr(out), st)
+    ms = _time_launches(fn, reps, device)
+    ok = bool(torch.equal(out[:4096], table[ids[:4096]]))   # bit-exact spot check
+    nbytes = ids.numel() * (8 + 2 * 4 * D)
+    gbs = nbytes / (ms / 1e3) / 1e9
+    del table, out
+    return {"kernel": "gather_rows_kernel", "workload": f"{n_titles} titles x {L} tokens, V={V}, D={D}",
+            "bound": "hbm", "ms": round(ms, 4), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+            "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": nbytes,
+            "traffic": load_traffic("gather"), "bit_exact_sample": ok}
+
+
+def news_encoder_cfg2(model, device, n_titles=100_000, reps=10):
+    """BASELINE config 2: NewsEncoder-only forward (get_news_vector) on 100k
+    synthetic titles; the folded Q|K|V vocabulary projection is recomputed on
+    every call (cache off), so each call does all of the encoder's work."""
+    gen = torch.Generator(device=device).manual_seed(6)
+    titles = synth_titles(gen, n_titles, V_WORDS, device)
+    from newsrecommendationsystem_amd import _native as Nat
+    cfg = model.news_encoder.config
+    saved = (cfg.hip_cache_folded_table, cfg.hip_proj_mode)
+    cfg.hip_cache_folded_table, cfg.hip_proj_mode = False, Nat.NRMS_PROJ_FOLDED
+    try:
+        with torch.no_grad():
+            ms = _time_launches(lambda: model.get_news_vector({"title": titles}), reps, device)
+    finally:
+        cfg.hip_cache_folded_table, cfg.hip_proj_mode = saved
+    return {"workload": f"BASELINE cfg2: NewsEncoder forward, {n_titles} titles x {L} tokens, "
+                        f"V={V_WORDS}, projection folded per call", "ms_per_call": round(ms, 4),
+            "titles_per_s": round(n_titles / (ms / 1e3), 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -145,6 +202,7 @@ def main():
     ap.add_argument("--proj", choices=["folded", "direct", "auto"], default="folded")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="separate MHSA / additive / pool kernels")
+    ap.add_argument("--no-extras", action="store_true", help="skip the gather / config-2 figures")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -230,6 +288,9 @@ def main():
         "stages_ms": {s: round(v, 4) for s, v in stage_ms.items()},
         "plan_equals_nrms_forward": same,
     }
+    if rank == 0 and world == 1 and not args.no_extras:
+        out["gather_roofline"] = gather_hbm(device)
+        out["news_encoder_cfg2"] = news_encoder_cfg2(model, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cb, parity = cpu_baseline(model, device)
         out["cpu_baseline"] = cb

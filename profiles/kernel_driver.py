@@ -28,6 +28,12 @@ def main():
     ap.add_argument("--unfused", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
+    if a.stage == "gather":   # isolated HBM gather figure (bench.gather_hbm)
+        for _ in range(a.iters):
+            bench.gather_hbm(dev, reps=1)
+        torch.cuda.synchronize()
+        print("ok", a.stage, a.iters)
+        return
     model = bench.build_model(dev)
     cand, clk = bench.synth_impressions(1000, 1024, bench.V_WORDS, dev)
     plan = ForwardPlan(model, 1024, bench.C, bench.N_CLICKED, bench.L, fused=not a.unfused)

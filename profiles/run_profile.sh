@@ -10,8 +10,13 @@ REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH=("$REPO/bench.py" --steps 20 --warmup 5 --no-cpu-baseline)
+BENCH=("$REPO/bench.py" --steps 20 --warmup 5 --no-cpu-baseline --no-extras)
+GATHER=("$REPO/profiles/kernel_driver.py" gather --iters 5)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" > "$OUT/bench_trace.json"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "${BENCH[@]}" > "$OUT/bench_fetch.json"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 "${BENCH[@]}" > "$OUT/bench_write.json"
+# the isolated gather (V = 1,048,576 table, config-2 shape) in the same three passes
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o gather -- python3 "${GATHER[@]}"
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o gather -- python3 "${GATHER[@]}"
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o gather -- python3 "${GATHER[@]}"
 find "$OUT" -name '*.csv' | sort

@@ -39,6 +39,8 @@ def stage_of(name, grid_threads, wg):
         return "score"
     if "fused_news" in name:
         return "news_fused"
+    if "gather_rows_kernel" in name:
+        return "gather"
     return None
 
 
@@ -53,7 +55,9 @@ def read_rows(path):
 
 
 def main(src, tag):
-    trace = read_rows(os.path.join(src, "trace", "run_kernel_trace.csv"))
+    import glob
+    trace = [r for p in sorted(glob.glob(os.path.join(src, "trace", "*_kernel_trace.csv")))
+             for r in read_rows(p)]
     dur = defaultdict(list)
     kname = {}
     for r in trace:
@@ -64,10 +68,9 @@ def main(src, tag):
 
     def counters(sub, cname):
         acc = defaultdict(list)
-        p = os.path.join(src, sub, "run_counter_collection.csv")
-        if not os.path.exists(p):
-            return acc
-        for r in read_rows(p):
+        rows = [r for p in sorted(glob.glob(os.path.join(src, sub, "*_counter_collection.csv")))
+                for r in read_rows(p)]
+        for r in rows:
             if r["Counter_Name"] != cname:
                 continue
             st = stage_of(r["Kernel_Name"], int(r["Grid_Size"]), int(r["Workgroup_Size"]))
@@ -99,6 +102,9 @@ def main(src, tag):
         json.dump(traffic, fo, indent=1)
     shutil.copy(os.path.join(src, "trace", "run_kernel_stats.csv"),
                 os.path.join(HERE, f"{tag}_kernel_stats.csv"))
+    g = os.path.join(src, "trace", "gather_kernel_stats.csv")
+    if os.path.exists(g):
+        shutil.copy(g, os.path.join(HERE, f"{tag}_gather_kernel_stats.csv"))
     print("\n".join(lines))
 
 
