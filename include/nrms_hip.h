@@ -110,8 +110,10 @@ int32_t nrms_additive_pool(const float* x, const float* scores, int64_t n_seq, i
                            int32_t D, float* out, hipStream_t stream);
 
 /* Fused NewsEncoder tail (news_encoder.py:42-47): raw-exp MHSA over projected
- * rows + additive attention + pooling, 4 titles per workgroup, the context
- * consumed from LDS by the additive GEMM. Row addressing as
+ * rows + additive attention + pooling, 4 titles per workgroup per step, all
+ * contractions on the matrix cores, the context kept in LDS for the additive
+ * GEMM and the pooling (workspace: only a packed copy of W_add). Row
+ * addressing as
  * nrms_self_attention. Compiled for the reference geometry (L = 20, D = 300,
  * H = 15, Q = 200); other shapes return NRMS_ERR_UNSUPPORTED (use the stage
  * entry points). Used by nrms_news_encode* and nrms_forward when it applies. */

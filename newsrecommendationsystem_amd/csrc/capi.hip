@@ -82,7 +82,7 @@ int32_t encode_from_qkv(const float* qkv, int64_t n_rows, const int64_t* ids_a, 
   const int D = w->d_model;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
     return launch_fused_news(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
-                             w->q_add, wap, ctx, out, s);
+                             w->q_add, wap, out, s);
   int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
   st = launch_gemm_additive_score(ctx, n_seq * L, D, w->w_add, w->b_add, w->q_add, w->query_dim,
@@ -170,7 +170,7 @@ int32_t nrms_additive_pool(const float* x, const float* scores, int64_t n_seq, i
 
 size_t nrms_news_attention_pool_workspace_size(int64_t n_titles, int32_t L, int32_t D) {
   if (n_titles < 0 || L <= 0 || D <= 0) return 0;
-  return align_up((size_t)n_titles * L * D * 4) + align_up(fused_news_packed_b_floats() * 4);
+  return align_up(fused_news_packed_b_floats() * 4);   // the context stays on chip
 }
 
 int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
@@ -183,11 +183,10 @@ int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int
   if (n_titles == 0) return NRMS_OK;
   if (!qkv || !out) return NRMS_ERR_INVALID_ARG;
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
-  float* ctx = cv.floats((size_t)n_titles * L * w->d_model);
   float* wap = cv.floats(fused_news_packed_b_floats());
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   return launch_fused_news(qkv, n_rows_qkv, tok_ids, n_seq_a, tok_ids_b, n_titles, w->w_add,
-                           w->b_add, w->q_add, wap, ctx, out, stream);
+                           w->b_add, w->q_add, wap, out, stream);
 }
 
 size_t nrms_news_encode_workspace_size(int64_t n_titles, int32_t L, int64_t V, int32_t D,

@@ -48,8 +48,9 @@ constexpr int FMT = FROWS / 16;      // 5 M tiles
 constexpr int SC = 328;              // context row stride in floats (== 8 mod 32)
 constexpr int NTHR = 256;
 constexpr int WAP_FLOATS = FKG * FNT * 64 * 4;             // packed Wa
-constexpr int SPECIAL_FLOATS = 2 * 3 * FD;                 // zero row + NaN row (q|k|v width)
-constexpr int LDS_FLOATS = FROWS * SC + 4 * FROWS + 2 * FROWS;   // ctx, partials, rowptr (u64)
+constexpr int ROW = 3 * FD;                                // q|k|v row: [q 300 | k 300 | v 300]
+constexpr int SPECIAL_FLOATS = 2 * ROW;                    // zero row + NaN row
+constexpr int LDS_FLOATS = FROWS * SC + 4 * FROWS + 2 * 2 * FROWS;   // ctx, partials, rowptr[2] (u64)
 constexpr size_t LDS_BYTES = LDS_FLOATS * sizeof(float);
 
 static_assert(FD == FH * FDK && FDK == 20 && FL == 20, "geometry");
@@ -64,7 +65,7 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= WAP_FLOATS + SPECIAL_FLOATS) return;
   if (idx >= WAP_FLOATS) {
-    WaP[idx] = (idx - WAP_FLOATS) < 3 * FD ? 0.f : qnan();
+    WaP[idx] = (idx - WAP_FLOATS) < ROW ? 0.f : qnan();
     return;
   }
   const int t = idx & 3;
@@ -90,6 +91,16 @@ struct RowMap {
   }
 };
 
+// Float offsets, within one q|k|v row, of what lane (head slot hl, x) of wave
+// (head group) g loads: q / k dims 4c..4c+3 of head h = 4g + hl, and v dims
+// 5x..5x+3 and 5x+4.
+struct QkvOffsets {
+  __device__ static int q(int g, int hl, int c) { return FDK * (4 * g + hl) + 4 * c; }
+  __device__ static int k(int g, int hl, int c) { return FD + FDK * (4 * g + hl) + 4 * c; }
+  __device__ static int v4(int g, int hl, int x) { return 2 * FD + FDK * (4 * g + hl) + 5 * x; }
+  __device__ static int v1(int g, int hl, int x) { return 2 * FD + FDK * (4 * g + hl) + 5 * x + 4; }
+};
+
 // 4 floats from a 4-byte-aligned address (V slices start at 5x floats).
 typedef float float4_a4 __attribute__((ext_vector_type(4), aligned(4)));
 // Row pointers come back from LDS as generic pointers; loads through them are
@@ -100,31 +111,72 @@ __device__ __forceinline__ const NRMS_GLOBAL T* gptr(const float* p) {
   return reinterpret_cast<const NRMS_GLOBAL T*>(reinterpret_cast<uintptr_t>(p));
 }
 
+// Phase timing (profiles/probes/fused_timing.hip builds with NRMS_FUSED_TIMING):
+// shader-cycle stamps accumulated per wave into dbg[wave][8].
+#ifdef NRMS_FUSED_TIMING
+#define NRMS_TIMING_PARAM , unsigned long long* __restrict__ dbg
+#define NRMS_STAMP(k)                                                 \
+  {                                                                   \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();     \
+    tacc[k] += now_ - tprev;                                          \
+    tprev = now_;                                                     \
+  }
+#else
+#define NRMS_TIMING_PARAM
+#define NRMS_STAMP(k)
+#endif
+
+// tanh(x) = 1 - 2 / (e^2x + 1): v_exp_f32 + v_rcp_f32, absolute error ~1e-7
+// over the whole range (the additive scores are sums of q_n tanh(.) with
+// |q_n| <= 0.1, so absolute error is what matters); saturates to +-1 and
+// propagates NaN.
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * x);   // e^(2x)
+  return fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
+}
+
+// Sum over the 16 lanes of a DPP row (all 16 get the total): quad butterflies,
+// then half-row and row mirrors. VALU only, no LDS crossbar round trips.
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));  // quad_perm [1,0,3,2]
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));  // quad_perm [2,3,0,1]
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false)); // row_half_mirror
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false)); // row_mirror
+  return v;
+}
+
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
 
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const float* __restrict__ qkv, RowMap rmap, int64_t n_groups, const float* __restrict__ WaP,
-    const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out) {
+    const float* __restrict__ b_add, const float* __restrict__ q_add,
+    float* __restrict__ out NRMS_TIMING_PARAM) {
+  using Off = QkvOffsets;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* ctxL = lds;                                   // [80][SC]
   float* part = ctxL + FROWS * SC;                     // [4][80] per-wave row partials
-  const float** rowptr = reinterpret_cast<const float**>(part + 4 * FROWS);   // [80]
+  const float** rowptr = reinterpret_cast<const float**>(part + 4 * FROWS);   // [2][80]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const float* zero_row = WaP + WAP_FLOATS;
-  const float* nan_row = zero_row + 3 * FD;
+  const float* nan_row = zero_row + ROW;
 
   // K padding: context columns 300..303 stay zero for the whole launch.
   if (tid < FROWS) *reinterpret_cast<float4*>(ctxL + tid * SC + FD) = make_float4(0.f, 0.f, 0.f, 0.f);
 
-  auto load_rows = [&](int64_t tg) {
-    if (tid < FROWS) {
-      const int t = tid / FL;
-      const int64_t row = rmap(tg * FT + t, tid - t * FL);
-      rowptr[tid] = row >= 0 ? qkv + row * (3 * FD) : (row == -1 ? nan_row : zero_row);
-    }
+  // row pointers of title group tg -> rowptr[buf]: the token id is loaded by
+  // row_of (threads < 80), the pointer stored later by store_row, so the id
+  // load's latency hides behind the work in between.
+  auto row_of = [&](int64_t tg) -> int64_t {
+    if (tid >= FROWS) return -2;
+    const int t = tid / FL;
+    return rmap(tg * FT + t, tid - t * FL);
+  };
+  auto store_row = [&](int64_t row, int buf) {
+    if (tid < FROWS)
+      rowptr[buf * FROWS + tid] = row >= 0 ? qkv + row * ROW : (row == -1 ? nan_row : zero_row);
   };
 
   // attention roles: block b = (title t, head slot hl), lane x within the block
@@ -132,7 +184,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   const int at = blk >> 2, hl = blk & 3;
   const int h = 4 * w + hl;
   const bool hval = h < FH;
-  const int hq = hval ? FDK * h : 0;
+  const int hls = hval ? hl : 0;   // the idle 16th head slot of wave 3 reads head 12
   // exp(d / sqrt(d_k)) as v_exp_f32(d * log2(e) / sqrt(d_k)): same overflow
   // (-> inf -> NaN) and underflow (-> 0) behaviour as the reference's exp.
   const float c_exp = 1.4426950408889634f / sqrtf((float)FDK);
@@ -152,34 +204,59 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   const float4* Bp = reinterpret_cast<const float4*>(WaP) + lane;
   const float* Aw = ctxL + lm * SC + 4 * kq;
 
-  if (blockIdx.x < n_groups) load_rows(blockIdx.x);
+  // q|k|v slices of one title group, lane (block (t, hl), x): Q / K of tokens
+  // x + 4j, V dims 5x..5x+4 of all 20 tokens. Loaded for the NEXT group at the
+  // start of the B epilogue, so the loads are in flight behind the tanh work,
+  // the pooling and two barriers instead of stalling the attention.
+  float qf[5][FDK], kf[5][FDK], vf[FL][5];
+  auto prefetch_qk = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      const float* rp = rowptr[buf * FROWS + FL * at + x + 4 * j];
+#pragma unroll
+      for (int c = 0; c < FDK / 4; ++c) {
+        const floatx4 a = *gptr<floatx4>(rp + Off::q(w, hls, c));
+        const floatx4 b = *gptr<floatx4>(rp + Off::k(w, hls, c));
+        qf[j][4 * c] = a.x; qf[j][4 * c + 1] = a.y; qf[j][4 * c + 2] = a.z; qf[j][4 * c + 3] = a.w;
+        kf[j][4 * c] = b.x; kf[j][4 * c + 1] = b.y; kf[j][4 * c + 2] = b.z; kf[j][4 * c + 3] = b.w;
+      }
+    }
+  };
+  // (50 + 40 loads in two batches: at most 63 may be outstanding per wave)
+  auto prefetch_v = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < FL; ++k) {
+      const float* vr = rowptr[buf * FROWS + FL * at + k];
+      const float4_a4 a = *gptr<float4_a4>(vr + Off::v4(w, hls, x));
+      vf[k][0] = a.x; vf[k][1] = a.y; vf[k][2] = a.z; vf[k][3] = a.w;
+      vf[k][4] = *gptr<float>(vr + Off::v1(w, hls, x));
+    }
+  };
 
-  for (int64_t tg = blockIdx.x; tg < n_groups; tg += gridDim.x) {
-    __syncthreads();   // rowptr of tg visible; context tile free (pooling of tg - grid done)
+  if (blockIdx.x < n_groups) store_row(row_of(blockIdx.x), 0);
+  __syncthreads();
+  if (blockIdx.x < n_groups) {
+    prefetch_qk(0);
+    prefetch_v(0);
+  }
+#ifdef NRMS_FUSED_TIMING
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = __builtin_amdgcn_s_memtime();
+#endif
+
+  int it = 0;
+  for (int64_t tg = blockIdx.x; tg < n_groups; tg += gridDim.x, ++it) {
+    const int nbuf = (it + 1) & 1;
+    __syncthreads();   // context tile free (pooling of the previous group done)
+    NRMS_STAMP(0)
 
     // ---------------- A: attention (4x4x1 MFMA, 16 (title, head) blocks) --------------
     {
-      float qf[5][FDK], kf[5][FDK], vf[FL][5];
-#pragma unroll
-      for (int j = 0; j < 5; ++j) {
-        const float* rp = rowptr[FL * at + x + 4 * j];
-        const NRMS_GLOBAL floatx4* qp = gptr<floatx4>(rp + hq);
-        const NRMS_GLOBAL floatx4* kp = gptr<floatx4>(rp + FD + hq);
-#pragma unroll
-        for (int c = 0; c < FDK / 4; ++c) {
-          const floatx4 a = qp[c], b = kp[c];
-          qf[j][4 * c] = a.x; qf[j][4 * c + 1] = a.y; qf[j][4 * c + 2] = a.z; qf[j][4 * c + 3] = a.w;
-          kf[j][4 * c] = b.x; kf[j][4 * c + 1] = b.y; kf[j][4 * c + 2] = b.z; kf[j][4 * c + 3] = b.w;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < FL; ++k) {
-        const float* vr = rowptr[FL * at + k] + 2 * FD + hq + 5 * x;
-        const NRMS_GLOBAL float* vp = gptr<float>(vr);
-        const float4_a4 a = *gptr<float4_a4>(vr);
-        vf[k][0] = a.x; vf[k][1] = a.y; vf[k][2] = a.z; vf[k][3] = a.w;
-        vf[k][4] = vp[4];
-      }
+      // row pointers of the next group, for the prefetch in this group's B
+      // epilogue (past the last group: zero rows, so the prefetch is
+      // unconditional and its registers are dead during the GEMM); stored at
+      // the end of this phase
+      const int64_t next_row = row_of(tg + gridDim.x);
       // S^T tiles: rows = keys 4j + r (A = K), cols = queries 4i + x (B = Q)
       floatx4 S[5][5];
 #pragma unroll
@@ -226,7 +303,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       if (hval) {
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-          float4* dst = reinterpret_cast<float4*>(ctxL + (FL * at + 4 * i + x) * SC + hq);
+          float4* dst = reinterpret_cast<float4*>(ctxL + (FL * at + 4 * i + x) * SC + FDK * h);
 #pragma unroll
           for (int c = 0; c < FDK / 4; ++c) {
             const int d0 = 4 * c;
@@ -235,8 +312,11 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           }
         }
       }
+      store_row(next_row, nbuf);
     }
+    NRMS_STAMP(1)
     __syncthreads();   // context tile complete
+    NRMS_STAMP(2)
 
     // ---------------- B: additive GEMM + tanh·q row partials ----------------
     {
@@ -272,6 +352,8 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           for (int j = 0; j < 4; ++j) bb[j] = bn[j];
         }
       }
+      NRMS_STAMP(3)
+      prefetch_qk(nbuf);
       // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
 #pragma unroll
       for (int mt = 0; mt < FMT; ++mt) {
@@ -279,18 +361,18 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         for (int r = 0; r < 4; ++r) {
           float p = 0.f;
 #pragma unroll
-          for (int j = 0; j < 3; ++j) p = fmaf(qv[j], tanhf(acc[mt][j][r] + bv[j]), p);
-          if (xok && mt == w) p = fmaf(qx, tanhf(accX[r] + bx), p);
-          if (xok && w == 0 && mt == FMT - 1) p = fmaf(qx, tanhf(accX2[r] + bx), p);
-          p += __shfl_xor(p, 1);
-          p += __shfl_xor(p, 2);
-          p += __shfl_xor(p, 4);
-          p += __shfl_xor(p, 8);
+          for (int j = 0; j < 3; ++j) p = fmaf(qv[j], tanh_fast(acc[mt][j][r] + bv[j]), p);
+          if (xok && mt == w) p = fmaf(qx, tanh_fast(accX[r] + bx), p);
+          if (xok && w == 0 && mt == FMT - 1) p = fmaf(qx, tanh_fast(accX2[r] + bx), p);
+          p = row16_sum(p);
           if (lm == 0) part[w * FROWS + 16 * mt + 4 * kq + r] = p;
         }
       }
+      prefetch_v(nbuf);
     }
+    NRMS_STAMP(4)
     __syncthreads();   // row partials complete
+    NRMS_STAMP(5)
 
     // ---------------- C: softmax over tokens + pooling (wave t <-> title t) ----------------
     {
@@ -325,9 +407,13 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         }
       }
       // rowptr of the next title group (its previous readers finished before the B barrier)
-      if (tg + gridDim.x < n_groups) load_rows(tg + gridDim.x);
     }
+    NRMS_STAMP(6)
   }
+#ifdef NRMS_FUSED_TIMING
+  if (lane == 0)
+    for (int k = 0; k < 8; ++k) dbg[(blockIdx.x * 4 + w) * 8 + k] = tacc[k];
+#endif
 }
 
 }  // namespace
@@ -338,15 +424,23 @@ bool fused_news_supported(int L, int D, int H, int Q) {
   return L == FL && D == FD && H == FH && Q == FQ;
 }
 
-int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
-                          const int64_t* ids_b, int64_t n_titles, const float* w_add,
-                          const float* b_add, const float* q_add, float* wap, float* /*ctx*/,
+#ifdef NRMS_FUSED_TIMING
+unsigned long long* g_fused_dbg = nullptr;   // set by profiles/probes/fused_timing.hip
+#define NRMS_TIMING_ARG , g_fused_dbg
+#else
+#define NRMS_TIMING_ARG
+#endif
+
+int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a,
+                          int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
+                          const float* w_add, const float* b_add, const float* q_add, float* wap,
                           float* out, hipStream_t s) {
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16) return NRMS_ERR_UNSUPPORTED;
+  auto kern = &fused_news_kernel;
   static bool attr_done = false;
   if (!attr_done) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_news_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
     attr_done = true;
   }
@@ -362,8 +456,8 @@ int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a
   }
   const int64_t blocks = n_groups < n_cu ? n_groups : n_cu;   // persistent: one workgroup per CU
   RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows};
-  hipLaunchKernelGGL(fused_news_kernel, dim3((unsigned)blocks), dim3(NTHR), LDS_BYTES, s, qkv, rm,
-                     n_groups, wap, b_add, q_add, out);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), LDS_BYTES, s, qkv, rm, n_groups,
+                     wap, b_add, q_add, out NRMS_TIMING_ARG);
   return launch_status();
 }
 

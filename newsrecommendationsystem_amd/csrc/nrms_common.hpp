@@ -81,9 +81,9 @@ int32_t launch_additive_pool(const float* x, const float* score, int64_t n_seq, 
                              float* out, hipStream_t s);
 size_t fused_news_packed_b_floats();
 bool fused_news_supported(int L, int D, int H, int Q);
-int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
-                          const int64_t* ids_b, int64_t n_titles, const float* w_add,
-                          const float* b_add, const float* q_add, float* wap, float* ctx,
+int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a,
+                          int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
+                          const float* w_add, const float* b_add, const float* q_add, float* wap,
                           float* out, hipStream_t s);
 int32_t launch_score_pairs(const float* news, int64_t n_news, const float* user, int64_t n_users,
                            const int64_t* news_idx, const int64_t* user_idx, int64_t n_pairs,
