@@ -103,6 +103,9 @@ __global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
   const float* Bw = Bs + lm * LDS_LD + 4 * kq;
 
   const int nk = (K + BK - 1) / BK;
+  // N tiles of this block that hold any column < N (the last column block of
+  // N = 900 has 3 empty tiles): the MFMAs of the others are skipped (uniform).
+  const int tn_valid = min(TN, (N - n0 + 15) / 16);
   gload(0);
   lstore();
   __syncthreads();
@@ -110,14 +113,16 @@ __global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
     if (kc + 1 < nk) gload(kc + 1);
 #pragma unroll
     for (int c = 0; c < BK / 16; ++c) {
+      if (kc * BK + 16 * c >= K) break;   // K tail: the zero-padded half chunk (K = 300)
       const float4 a0 = *reinterpret_cast<const float4*>(Aw + 16 * c);
       const float4 a1 = *reinterpret_cast<const float4*>(Aw + 16 * LDS_LD + 16 * c);
       // B fragments two column tiles at a time: 4 independent accumulators per
       // k-step keep the MFMA pipe busy without holding all TN fragments live.
 #pragma unroll
       for (int tn = 0; tn < TN; tn += 2) {
+        if (tn >= tn_valid) break;
         const float4 b0 = *reinterpret_cast<const float4*>(Bw + tn * 16 * LDS_LD + 16 * c);
-        if (tn + 1 < TN) {
+        if (tn + 1 < TN && tn + 1 < tn_valid) {
           const float4 b1 = *reinterpret_cast<const float4*>(Bw + (tn + 1) * 16 * LDS_LD + 16 * c);
 #define NRMS_MFMA4(F)                                                                             \
   acc[0][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.F, b0.F, acc[0][tn], 0, 0, 0);             \
