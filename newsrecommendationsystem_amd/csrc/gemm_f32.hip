@@ -24,21 +24,17 @@ constexpr int kThreads = 256;
 // K-permutation: MFMA step (c, t) gives lane group kq (= lane >> 4) the K index
 // 16c + 4kq + t, so each lane fetches its four consecutive K values with one
 // ds_read_b128; A and B use the same map, so every K term is summed once.
+// One 128 x (16 TN) output tile at (m0, n0); As / Bs are the workgroup's LDS
+// tiles (declared once by the kernel so both tile widths share them).
 template <int TN, bool ADDITIVE>
-__global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
+__device__ __forceinline__ void gemm_tile(
     const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
-    int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy,
-    const float* __restrict__ qvec, float* __restrict__ score, int n_col_tiles) {
+    int64_t M, int K, const WeightRows& wr, int N, float* __restrict__ Y, int64_t ldy,
+    const float* __restrict__ qvec, float* __restrict__ score, int64_t m0, int n0,
+    float* __restrict__ As, float* __restrict__ Bs) {
   constexpr int BN = 16 * TN;
   constexpr int A_PASSES = BM * BK / 4 / kThreads;              // 4
   constexpr int B_PASSES = (BN * BK / 4 + kThreads - 1) / kThreads;
-  __shared__ __attribute__((aligned(16))) float As[BM * LDS_LD];
-  __shared__ __attribute__((aligned(16))) float Bs[BN * LDS_LD];
-
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
-  const int ct = wg % n_col_tiles;
-  const int64_t m0 = (int64_t)(wg / n_col_tiles) * BM;
-  const int n0 = ct * BN;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -103,9 +99,6 @@ __global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
   const float* Bw = Bs + lm * LDS_LD + 4 * kq;
 
   const int nk = (K + BK - 1) / BK;
-  // N tiles of this block that hold any column < N (the last column block of
-  // N = 900 has 3 empty tiles): the MFMAs of the others are skipped (uniform).
-  const int tn_valid = min(TN, (N - n0 + 15) / 16);
   gload(0);
   lstore();
   __syncthreads();
@@ -120,9 +113,8 @@ __global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
       // k-step keep the MFMA pipe busy without holding all TN fragments live.
 #pragma unroll
       for (int tn = 0; tn < TN; tn += 2) {
-        if (tn >= tn_valid) break;
         const float4 b0 = *reinterpret_cast<const float4*>(Bw + tn * 16 * LDS_LD + 16 * c);
-        if (tn + 1 < TN && tn + 1 < tn_valid) {
+        if (tn + 1 < TN) {
           const float4 b1 = *reinterpret_cast<const float4*>(Bw + (tn + 1) * 16 * LDS_LD + 16 * c);
 #define NRMS_MFMA4(F)                                                                             \
   acc[0][tn] = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.F, b0.F, acc[0][tn], 0, 0, 0);             \
@@ -190,7 +182,28 @@ __global__ __launch_bounds__(kThreads) void gemm_xwt_f32_kernel(
   }
 }
 
-constexpr int TN_STORE = 12;     // BN = 192: N = 900 -> 5 column tiles
+// Column tiles of width 16 TN; when N is not a multiple of 16 TN the last
+// column tile is TNT tiles wide (N = 900: 4 x 192 + 1 x 144), so no MFMA is
+// spent on all-padding columns.
+template <int TN, int TNT, bool ADDITIVE>
+__global__ __launch_bounds__(kThreads, 2) void gemm_xwt_f32_kernel(
+    const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
+    int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy,
+    const float* __restrict__ qvec, float* __restrict__ score, int n_col_tiles) {
+  __shared__ __attribute__((aligned(16))) float As[BM * LDS_LD];
+  __shared__ __attribute__((aligned(16))) float Bs[16 * TN * LDS_LD];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int ct = wg % n_col_tiles;
+  const int64_t m0 = (int64_t)(wg / n_col_tiles) * BM;
+  const int n0 = ct * 16 * TN;
+  if (TNT == TN || n0 + 16 * TN <= N)
+    gemm_tile<TN, ADDITIVE>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, qvec, score, m0, n0, As, Bs);
+  else
+    gemm_tile<TNT, ADDITIVE>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, qvec, score, m0, n0, As, Bs);
+}
+
+constexpr int TN_STORE = 12;     // BN = 192: N = 900 -> 4 column tiles of 192 + one of 144
+constexpr int TN_STORE_TAIL = 9;
 constexpr int TN_ADDITIVE = 13;  // BN = 208 >= Q = 200: one column tile
 
 }  // namespace
@@ -206,9 +219,17 @@ int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_i
   const int64_t nrt = (M + BM - 1) / BM;
   const int64_t blocks = nrt * nct;
   if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, false>), dim3((unsigned)blocks),
-                     dim3(kThreads), 0, s, X, n_rows_x, row_ids, M, K, w, N, Y, ldy,
-                     (const float*)nullptr, (float*)nullptr, nct);
+  // the narrow last tile covers N = 900's remainder (132 columns); for other N
+  // fall back to full-width tiles
+  const int rem = N % (16 * TN_STORE);
+  if (rem > 0 && rem <= 16 * TN_STORE_TAIL)
+    hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, TN_STORE_TAIL, false>), dim3((unsigned)blocks),
+                       dim3(kThreads), 0, s, X, n_rows_x, row_ids, M, K, w, N, Y, ldy,
+                       (const float*)nullptr, (float*)nullptr, nct);
+  else
+    hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, TN_STORE, false>), dim3((unsigned)blocks),
+                       dim3(kThreads), 0, s, X, n_rows_x, row_ids, M, K, w, N, Y, ldy,
+                       (const float*)nullptr, (float*)nullptr, nct);
   return launch_status();
 }
 
@@ -226,7 +247,7 @@ int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float
   w.nseg = 1;
   const int64_t blocks = (M + BM - 1) / BM;
   if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_ADDITIVE, true>), dim3((unsigned)blocks),
+  hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_ADDITIVE, TN_ADDITIVE, true>), dim3((unsigned)blocks),
                      dim3(kThreads), 0, s, X, M, (const int64_t*)nullptr, M, K, w, N,
                      (float*)nullptr, (int64_t)0, q, score, 1);
   return launch_status();
