@@ -203,6 +203,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="separate MHSA / additive / pool kernels")
     ap.add_argument("--no-extras", action="store_true", help="skip the gather / config-2 figures")
+    ap.add_argument("--gemm", choices=["x6", "f32"], default="x6",
+                    help="GEMM arithmetic: split-bf16 x6 (fp32-accurate, default) or exact f32 MFMA")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,6 +222,7 @@ def main():
     from newsrecommendationsystem_amd import _native as Nat
     from newsrecommendationsystem_amd.pipeline import ForwardPlan
 
+    Nat.load().nrms_set_gemm_arith(Nat.NRMS_GEMM_SPLIT_BF16X6 if args.gemm == "x6" else Nat.NRMS_GEMM_F32)
     mode = {"folded": Nat.NRMS_PROJ_FOLDED, "direct": Nat.NRMS_PROJ_DIRECT, "auto": Nat.NRMS_PROJ_AUTO}[args.proj]
     model = build_model(device)
     B = args.batch
@@ -273,13 +276,14 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "impressions/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32" if args.gemm == "f32" else "fp32 (GEMMs: exact 3-way bf16 split, 6 products, fp32 accumulate)",
         "data": "synthetic (MIND-shaped ids, random-init weights, N(0,1) embedding table)",
         "config": {"workload": "BASELINE cfg3: full NRMS forward scoring (news+user encoder+"
                                "click predictor), every title encoded", "global_batch": B * world,
                    "impressions_per_gpu": B, "candidates": C, "clicked": N_CLICKED,
                    "title_len": L, "vocab": V_WORDS, "d_model": D, "heads": 15,
-                   "query_dim": 200, "proj_mode": args.proj, "news_tail": "unfused" if args.unfused else "fused",
+                   "query_dim": 200, "proj_mode": args.proj, "gemm_arith": args.gemm, "news_tail": "unfused" if args.unfused else "fused",
                    "parallelism": f"user-shard x{world}"},
         "roofline": {"kernel": dom, "bound": bound, "achieved": round(achieved, 3),
                      "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),

@@ -67,6 +67,22 @@ typedef struct {
  * the batch has more tokens than the vocabulary. */
 typedef enum { NRMS_PROJ_AUTO = 0, NRMS_PROJ_DIRECT = 1, NRMS_PROJ_FOLDED = 2 } nrms_proj_mode_t;
 
+/* Arithmetic of the matrix-core GEMMs (Q|K|V projections and the news
+ * encoder's additive projection; attention contractions are always f32 MFMA).
+ * SPLIT_BF16X6 (default): each fp32 operand is split exactly into three bf16
+ * planes (hi + mid + lo, 8 significand bits each) and the six plane products
+ * with i + j <= 2 are accumulated in fp32 on v_mfma_f32_16x16x32_bf16; every
+ * bf16 product is exact and the dropped terms are below 2^-25 |a||b|, so the
+ * result has fp32-GEMM accuracy (measured: normwise error vs fp64 at or below
+ * the F32 mode's) at 6/16 of the f32-MFMA cycles. F32: v_mfma_f32_16x16x4_f32,
+ * each product an exact fp32 FMA. Process-wide; the initial value comes from
+ * the environment (NRMS_GEMM=f32 selects F32). Returns the previous mode, or
+ * -NRMS_ERR_INVALID_ARG for an unknown mode. Not synchronised with launches
+ * in flight: set it before enqueuing work. */
+typedef enum { NRMS_GEMM_SPLIT_BF16X6 = 0, NRMS_GEMM_F32 = 1 } nrms_gemm_arith_t;
+int32_t nrms_set_gemm_arith(int32_t mode);
+int32_t nrms_get_gemm_arith(void);
+
 int32_t nrms_abi_version(void);
 const char* nrms_status_string(int32_t status);
 int32_t nrms_last_hip_error(void);

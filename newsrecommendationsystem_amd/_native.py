@@ -15,6 +15,8 @@ LIB_PATH = os.path.join(_PKG, "libnrms_hip.so")
 ABI_VERSION = 1
 
 NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
+NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32 = 0, 1
+GEMM_ARITH_NAMES = {NRMS_GEMM_SPLIT_BF16X6: "split-bf16x6", NRMS_GEMM_F32: "f32"}
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32
@@ -34,6 +36,8 @@ _EW = ctypes.POINTER(EncoderWeights)
 # name -> (restype, argtypes)
 SIGNATURES = {
     "nrms_abi_version": (_i32, []),
+    "nrms_set_gemm_arith": (_i32, [_i32]),
+    "nrms_get_gemm_arith": (_i32, []),
     "nrms_status_string": (ctypes.c_char_p, [_i32]),
     "nrms_last_hip_error": (_i32, []),
     "nrms_embedding_gather": (_i32, [_p, _i64, _p, _i64, _i32, _p, _p]),
@@ -106,3 +110,22 @@ def ptr(t):
 
 def stream_handle(device=None):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class gemm_arith:
+    """Context manager selecting the GEMM arithmetic (nrms_set_gemm_arith) for
+    the enclosed calls; restores the previous mode on exit."""
+
+    def __init__(self, mode):
+        self.mode = mode
+
+    def __enter__(self):
+        prev = load().nrms_set_gemm_arith(self.mode)
+        if prev < 0:
+            raise NativeError(f"unknown GEMM arithmetic {self.mode}")
+        self.prev = prev
+        return self
+
+    def __exit__(self, *exc):
+        load().nrms_set_gemm_arith(self.prev)
+        return False

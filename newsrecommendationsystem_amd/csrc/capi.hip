@@ -3,10 +3,20 @@
 // on the caller's stream (no allocation, no synchronisation).
 #include "nrms_common.hpp"
 
+#include <atomic>
+#include <cstdlib>
+
 namespace nrms {
 
 static thread_local int32_t g_last_hip = 0;
 void set_last_hip_error(hipError_t e) { g_last_hip = (int32_t)e; }
+
+static int initial_gemm_arith() {
+  const char* e = getenv("NRMS_GEMM");
+  return (e && (e[0] == 'f' || e[0] == 'F')) ? NRMS_GEMM_F32 : NRMS_GEMM_SPLIT_BF16X6;
+}
+static std::atomic<int> g_gemm_arith{initial_gemm_arith()};
+int gemm_arith() { return g_gemm_arith.load(std::memory_order_relaxed); }
 
 namespace {
 
@@ -99,6 +109,13 @@ using namespace nrms;
 extern "C" {
 
 int32_t nrms_abi_version(void) { return NRMS_ABI_VERSION; }
+
+int32_t nrms_set_gemm_arith(int32_t mode) {
+  if (mode != NRMS_GEMM_SPLIT_BF16X6 && mode != NRMS_GEMM_F32) return -NRMS_ERR_INVALID_ARG;
+  return g_gemm_arith.exchange(mode);
+}
+
+int32_t nrms_get_gemm_arith(void) { return gemm_arith(); }
 
 const char* nrms_status_string(int32_t st) {
   switch (st) {

@@ -202,6 +202,194 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_xwt_f32_kernel(
     gemm_tile<TNT, ADDITIVE>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, qvec, score, m0, n0, As, Bs);
 }
 
+// ---------------------------------------------------------------------------
+// Split-bf16 (x6) variant of the store GEMM: every fp32 operand is split into
+// hi + mid + lo bf16 planes (exact: 8 + 8 + 8 significand bits) while it is
+// staged into LDS, and each 16x16 output tile accumulates the six products
+// with plane indices i + j <= 2 on v_mfma_f32_16x16x32_bf16 (exact bf16
+// products, fp32 accumulation). Dropped terms are < 2^-25 |a||b| per product:
+// fp32-GEMM accuracy (tests compare against the fp64 oracle) at 6/16 of the
+// f32-MFMA cycles.
+// Block tile 128 x 192, K staged 32 deep (one bf16 k-step) with register
+// prefetch of the next chunk; 4 waves as 2 (rows) x 2 (cols), wave tile
+// 64 x (16 TNW); two workgroups per CU so one stages while the other computes.
+constexpr int XBM = 128;
+constexpr int XBK = 32;
+constexpr int XLD = 40;   // bf16 per LDS row: 80 B = 16 x 5, conflict-free ds_read_b128 fragments
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split4(const float4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
+  const float x[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const __bf16 a = (__bf16)x[e];
+    const float r = x[e] - (float)a;
+    const __bf16 b = (__bf16)r;
+    h[e] = a;
+    m[e] = b;
+    l[e] = (__bf16)(r - (float)b);
+  }
+}
+
+template <int TNW>
+__device__ __forceinline__ void gemm_x6_tile(
+    const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
+    int64_t M, int K, const WeightRows& wr, int N, float* __restrict__ Y, int64_t ldy,
+    int64_t m0, int n0, __bf16* __restrict__ As, __bf16* __restrict__ Bs) {
+  constexpr int BN = 32 * TNW;
+  constexpr int A_PASSES = XBM * XBK / 4 / kThreads;              // 4
+  constexpr int B_PASSES = (BN * XBK / 4 + kThreads - 1) / kThreads;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;
+  const int lrow = tid >> 3, lc4 = tid & 7;
+
+  const float* a_src[A_PASSES];
+  bool a_bad[A_PASSES];
+#pragma unroll
+  for (int p = 0; p < A_PASSES; ++p) {
+    const int64_t m = m0 + lrow + 32 * p;
+    a_src[p] = nullptr;
+    a_bad[p] = false;
+    if (m < M) {
+      const int64_t r = row_ids ? row_ids[m] : m;
+      if ((uint64_t)r < (uint64_t)n_rows_x) a_src[p] = X + r * K;
+      else a_bad[p] = true;  // invalid id: the row becomes NaN
+    }
+  }
+  const float* b_src[B_PASSES];
+#pragma unroll
+  for (int p = 0; p < B_PASSES; ++p) {
+    const int n = n0 + lrow + 32 * p;
+    b_src[p] = nullptr;
+    if (lrow + 32 * p < BN && n < N) {
+      const int seg = n / wr.seg_rows;
+      b_src[p] = wr.w[seg] + (int64_t)(n - seg * wr.seg_rows) * K;
+    }
+  }
+
+  float4 ra[A_PASSES], rb[B_PASSES];
+  auto gload = [&](int kc) {
+    const int k = kc * XBK + lc4 * 4;
+    const bool kin = k < K;
+#pragma unroll
+    for (int p = 0; p < A_PASSES; ++p)
+      ra[p] = (a_src[p] && kin) ? *reinterpret_cast<const float4*>(a_src[p] + k)
+                                : (a_bad[p] ? nan4() : make_float4(0.f, 0.f, 0.f, 0.f));
+#pragma unroll
+    for (int p = 0; p < B_PASSES; ++p)
+      rb[p] = (b_src[p] && kin) ? *reinterpret_cast<const float4*>(b_src[p] + k)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int p = 0; p < A_PASSES; ++p) {
+      bf16x4 h, m, l;
+      split4(ra[p], h, m, l);
+      __bf16* d = As + (lrow + 32 * p) * XLD + lc4 * 4;
+      *reinterpret_cast<bf16x4*>(d) = h;
+      *reinterpret_cast<bf16x4*>(d + XBM * XLD) = m;
+      *reinterpret_cast<bf16x4*>(d + 2 * XBM * XLD) = l;
+    }
+#pragma unroll
+    for (int p = 0; p < B_PASSES; ++p)
+      if (lrow + 32 * p < BN) {
+        bf16x4 h, m, l;
+        split4(rb[p], h, m, l);
+        __bf16* d = Bs + (lrow + 32 * p) * XLD + lc4 * 4;
+        *reinterpret_cast<bf16x4*>(d) = h;
+        *reinterpret_cast<bf16x4*>(d + BN * XLD) = m;
+        *reinterpret_cast<bf16x4*>(d + 2 * BN * XLD) = l;
+      }
+  };
+
+  floatx4 acc[4][TNW];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int nt = 0; nt < TNW; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
+  // N tiles of this wave past N hold no output: skip their MFMAs (wave-uniform)
+  int nt_live = TNW;
+  {
+    const int first = n0 + 16 * TNW * wn;
+    const int live = (N - first + 15) / 16;
+    nt_live = live < 0 ? 0 : (live < TNW ? live : TNW);
+  }
+
+  const int lm = lane & 15, kq = lane >> 4;
+  const __bf16* Aw = As + (64 * wm + lm) * XLD + 8 * kq;
+  const __bf16* Bw = Bs + (16 * TNW * wn + lm) * XLD + 8 * kq;
+
+  const int nk = (K + XBK - 1) / XBK;
+  gload(0);
+  lstore();
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    if (kc + 1 < nk) gload(kc + 1);
+    bf16x8 a[4][3];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        a[mt][pl] = *reinterpret_cast<const bf16x8*>(Aw + pl * XBM * XLD + 16 * mt * XLD);
+#pragma unroll
+    for (int nt = 0; nt < TNW; ++nt) {
+      if (nt >= nt_live) break;
+      bf16x8 b[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[pl] = *reinterpret_cast<const bf16x8*>(Bw + pl * BN * XLD + 16 * nt * XLD);
+      // the six products with i + j <= 2, smallest first
+#define NRMS_X6(PA, PB)                                                                             \
+  _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                                  \
+      acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], b[PB], acc[mt][nt], 0, 0, 0);
+      NRMS_X6(2, 0) NRMS_X6(1, 1) NRMS_X6(0, 2) NRMS_X6(1, 0) NRMS_X6(0, 1) NRMS_X6(0, 0)
+#undef NRMS_X6
+    }
+    __syncthreads();
+    if (kc + 1 < nk) {
+      lstore();
+      __syncthreads();
+    }
+  }
+
+  // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
+  const int64_t row_base = m0 + 64 * wm + kq * 4;
+#pragma unroll
+  for (int nt = 0; nt < TNW; ++nt) {
+    const int col = n0 + 16 * TNW * wn + 16 * nt + lm;
+    if (col >= N) continue;
+    const int seg = col / wr.seg_rows;
+    const float bias = wr.b[seg][col - seg * wr.seg_rows];
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row_base + 16 * mt + r;
+        if (row < M) Y[row * ldy + col] = acc[mt][nt][r] + bias;
+      }
+  }
+}
+
+// 192-wide column tiles; a last partial tile of <= 160 columns (N = 900:
+// 4 x 192 + 132) runs the 160-wide instantiation so its two wave columns
+// stay balanced (5 + 4 live N tiles instead of 6 + 3).
+__global__ __launch_bounds__(kThreads, 2) void gemm_x6_kernel(
+    const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
+    int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy, int n_col_tiles) {
+  __shared__ __attribute__((aligned(16))) __bf16 As[3 * XBM * XLD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * 192 * XLD];
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int ct = wg % n_col_tiles;
+  const int64_t m0 = (int64_t)(wg / n_col_tiles) * XBM;
+  const int n0 = ct * 192;
+  if (N - n0 > 160)
+    gemm_x6_tile<6>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
+  else
+    gemm_x6_tile<5>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
+}
+
 constexpr int TN_STORE = 12;     // BN = 192: N = 900 -> 4 column tiles of 192 + one of 144
 constexpr int TN_STORE_TAIL = 9;
 constexpr int TN_ADDITIVE = 13;  // BN = 208 >= Q = 200: one column tile
@@ -215,6 +403,17 @@ int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_i
   if (K % 4 != 0 || ((uintptr_t)X % 16) != 0) return NRMS_ERR_UNSUPPORTED;
   for (int i = 0; i < w.nseg; ++i)
     if (((uintptr_t)w.w[i] % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  if (gemm_arith() == NRMS_GEMM_SPLIT_BF16X6) {
+    // 192-wide column tiles; a last partial tile of <= 160 columns runs the
+    // TNW = 5 instantiation (N = 900: 4 x 192 + 132)
+    const int nct = (N + 191) / 192;
+    const int64_t nrt = (M + XBM - 1) / XBM;
+    const int64_t blocks = nrt * nct;
+    if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(gemm_x6_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, X, n_rows_x,
+                       row_ids, M, K, w, N, Y, ldy, nct);
+    return launch_status();
+  }
   const int nct = (N + 16 * TN_STORE - 1) / (16 * TN_STORE);
   const int64_t nrt = (M + BM - 1) / BM;
   const int64_t blocks = nrt * nct;

@@ -53,6 +53,31 @@ constexpr int SPECIAL_FLOATS = 2 * ROW;                    // zero row + NaN row
 constexpr int LDS_FLOATS = FROWS * SC + 4 * FROWS + 2 * 2 * FROWS;   // ctx, partials, rowptr[2] (u64)
 constexpr size_t LDS_BYTES = LDS_FLOATS * sizeof(float);
 
+// Split-bf16 GEMM variant (X6): the context is stored as three bf16 planes
+// hi | mid | lo with hi + mid + lo == ctx exactly (8 + 8 + 8 significand
+// bits, each residual exact in fp32), and Wa likewise; the additive GEMM sums
+// the six products with i + j <= 2 on v_mfma_f32_16x16x32_bf16 (exact bf16
+// products, fp32 accumulation). The dropped terms are < 2^-25 |a||b|, below
+// one fp32 rounding: the result is as accurate as an fp32 GEMM (tested against
+// the fp64 oracle) at 6/16 of the f32-MFMA time.
+constexpr int XKS = 10;                   // k-steps of 32 (K = 300 padded to 320)
+constexpr int XKP = XKS * 32;             // 320
+constexpr int XRB = 3 * XKP + 8;          // row stride in bf16 (1936 B = 16 x 121: conflict-free b128 rows)
+constexpr int WAP3_FLOATS = XKS * FNT * 3 * 64 * 4;   // [ks][nt][plane][lane][8 bf16]
+constexpr int WAP_MAX = WAP3_FLOATS > WAP_FLOATS ? WAP3_FLOATS : WAP_FLOATS;
+constexpr size_t LDS_BYTES_X6 = (size_t)FROWS * XRB * 2 + (4 * FROWS + 2 * 2 * FROWS) * sizeof(float);
+static_assert(LDS_BYTES_X6 <= 160 * 1024, "LDS (x6)");
+static_assert((FROWS * XRB * 2) % 16 == 0 && (XRB * 2) % 32 == 16, "x6 row stride");
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)x;
+  const float r = x - (float)hi;
+  mid = (__bf16)r;
+  lo = (__bf16)(r - (float)mid);
+}
+
 static_assert(FD == FH * FDK && FDK == 20 && FL == 20, "geometry");
 static_assert(FKG * 16 >= FD && SC >= FKG * 16, "K padding");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS");
@@ -65,7 +90,8 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= WAP_FLOATS + SPECIAL_FLOATS) return;
   if (idx >= WAP_FLOATS) {
-    WaP[idx] = (idx - WAP_FLOATS) < ROW ? 0.f : qnan();
+    const int sidx = idx - WAP_FLOATS;
+    WaP[WAP_MAX + sidx] = sidx < ROW ? 0.f : qnan();
     return;
   }
   const int t = idx & 3;
@@ -75,6 +101,29 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
   const int n = 16 * nt + (lane & 15);
   const int k = 16 * c + 4 * (lane >> 4) + t;
   WaP[idx] = (n < FQ && k < FD) ? Wa[n * FD + k] : 0.f;
+}
+
+// X6: WaP3[ks][nt][plane][lane][8] bf16 = plane of Wa[16 nt + (lane & 15)][32 ks + 8 (lane >> 4) + i]
+// (the B-operand fragments of v_mfma_f32_16x16x32_bf16), zero past Q or D.
+__global__ __launch_bounds__(256) void pack_additive_b3_kernel(const float* __restrict__ Wa,
+                                                               float* __restrict__ WaP) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  constexpr int NE = XKS * FNT * 64 * 8;
+  if (idx >= NE + SPECIAL_FLOATS) return;
+  if (idx >= NE) {
+    const int sidx = idx - NE;
+    WaP[WAP_MAX + sidx] = sidx < ROW ? 0.f : qnan();
+    return;
+  }
+  const int i = idx & 7, lane = (idx >> 3) & 63, nt = (idx >> 9) % FNT, ks = (idx >> 9) / FNT;
+  const int n = 16 * nt + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + i;
+  const float v = (n < FQ && k < FD) ? Wa[n * FD + k] : 0.f;
+  __bf16 hi, mid, lo;
+  split3(v, hi, mid, lo);
+  __bf16* o = reinterpret_cast<__bf16*>(WaP) + (((ks * FNT + nt) * 3) * 64 + lane) * 8 + i;
+  o[0] = hi;
+  o[64 * 8] = mid;
+  o[2 * 64 * 8] = lo;
 }
 
 struct RowMap {
@@ -149,22 +198,34 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
 
+template <bool X6>
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const float* __restrict__ qkv, RowMap rmap, int64_t n_groups, const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add,
     float* __restrict__ out NRMS_TIMING_PARAM) {
   using Off = QkvOffsets;
   extern __shared__ __attribute__((aligned(16))) float lds[];
-  float* ctxL = lds;                                   // [80][SC]
-  float* part = ctxL + FROWS * SC;                     // [4][80] per-wave row partials
+  float* ctxL = lds;                                   // f32: [80][SC]
+  __bf16* ctxB = reinterpret_cast<__bf16*>(lds);       // x6:  [80][XRB] = hi | mid | lo planes
+  float* part = X6 ? lds + FROWS * XRB / 2 : ctxL + FROWS * SC;   // [4][80] per-wave row partials
   const float** rowptr = reinterpret_cast<const float**>(part + 4 * FROWS);   // [2][80]
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const float* zero_row = WaP + WAP_FLOATS;
+  const float* zero_row = WaP + WAP_MAX;
   const float* nan_row = zero_row + ROW;
 
-  // K padding: context columns 300..303 stay zero for the whole launch.
-  if (tid < FROWS) *reinterpret_cast<float4*>(ctxL + tid * SC + FD) = make_float4(0.f, 0.f, 0.f, 0.f);
+  // K padding: context columns 300..303 (x6: 300..319 of every plane) stay zero for the whole launch.
+  if (tid < FROWS) {
+    if constexpr (X6) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int c = 0; c < (XKP - FD) / 4; ++c)
+          *reinterpret_cast<uint2*>(ctxB + tid * XRB + pl * XKP + FD + 4 * c) = make_uint2(0u, 0u);
+    } else {
+      *reinterpret_cast<float4*>(ctxL + tid * SC + FD) = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  }
 
   // row pointers of title group tg -> rowptr[buf]: the token id is loaded by
   // row_of (threads < 80), the pointer stored later by store_row, so the id
@@ -303,12 +364,30 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       if (hval) {
 #pragma unroll
         for (int i = 0; i < 5; ++i) {
-          float4* dst = reinterpret_cast<float4*>(ctxL + (FL * at + 4 * i + x) * SC + FDK * h);
+          if constexpr (X6) {
+            __bf16* dst = ctxB + (FL * at + 4 * i + x) * XRB + FDK * h;
 #pragma unroll
-          for (int c = 0; c < FDK / 4; ++c) {
-            const int d0 = 4 * c;
-            dst[c] = make_float4(O[d0 % 5][i][d0 / 5], O[(d0 + 1) % 5][i][(d0 + 1) / 5],
-                                 O[(d0 + 2) % 5][i][(d0 + 2) / 5], O[(d0 + 3) % 5][i][(d0 + 3) / 5]);
+            for (int c = 0; c < FDK / 4; ++c) {
+              bf16x4 vh, vm, vl;
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const int d = 4 * c + e;
+                __bf16 a, b, cc;
+                split3(O[d % 5][i][d / 5], a, b, cc);
+                vh[e] = a; vm[e] = b; vl[e] = cc;
+              }
+              *reinterpret_cast<bf16x4*>(dst + 4 * c) = vh;
+              *reinterpret_cast<bf16x4*>(dst + XKP + 4 * c) = vm;
+              *reinterpret_cast<bf16x4*>(dst + 2 * XKP + 4 * c) = vl;
+            }
+          } else {
+            float4* dst = reinterpret_cast<float4*>(ctxL + (FL * at + 4 * i + x) * SC + FDK * h);
+#pragma unroll
+            for (int c = 0; c < FDK / 4; ++c) {
+              const int d0 = 4 * c;
+              dst[c] = make_float4(O[d0 % 5][i][d0 / 5], O[(d0 + 1) % 5][i][(d0 + 1) / 5],
+                                   O[(d0 + 2) % 5][i][(d0 + 2) / 5], O[(d0 + 3) % 5][i][(d0 + 3) / 5]);
+            }
           }
         }
       }
@@ -325,6 +404,49 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       for (int mt = 0; mt < FMT; ++mt)
 #pragma unroll
         for (int j = 0; j < 3; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (X6) {
+        // A fragments (16x16x32): lane holds A[row lm][32 ks + 8 kq .. + 7] of each plane
+        const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
+        const __bf16* Ab = ctxB + lm * XRB + 8 * kq;
+        bf16x8 bb[4][3], bn[4][3];
+        auto load_b = [&](int ks, bf16x8 (&dst)[4][3]) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int nt = j < 3 ? 3 * w + j : 12;
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl) dst[j][pl] = Bq[((ks * FNT + nt) * 3 + pl) * 64];
+          }
+        };
+        load_b(0, bb);
+        for (int ks = 0; ks < XKS; ++ks) {
+          if (ks + 1 < XKS) load_b(ks + 1, bn);
+          bf16x8 a[FMT][3], ax[3];
+#pragma unroll
+          for (int mt = 0; mt < FMT; ++mt)
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+              a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * XRB + pl * XKP + 32 * ks);
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            ax[pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * w * XRB + pl * XKP + 32 * ks);
+          // the six products with i + j <= 2, smallest first
+#define NRMS_X6STEP(PA, PB)                                                                              \
+  _Pragma("unroll") for (int mt = 0; mt < FMT; ++mt)                                                     \
+  _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                          \
+      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);   \
+  accX = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[PA], bb[3][PB], accX, 0, 0, 0);                      \
+  if (w == 0) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[FMT - 1][PA], bb[3][PB], accX2, 0, 0, 0);
+          NRMS_X6STEP(2, 0) NRMS_X6STEP(1, 1) NRMS_X6STEP(0, 2) NRMS_X6STEP(1, 0) NRMS_X6STEP(0, 1)
+          NRMS_X6STEP(0, 0)
+#undef NRMS_X6STEP
+          if (ks + 1 < XKS) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int pl = 0; pl < 3; ++pl) bb[j][pl] = bn[j][pl];
+          }
+        }
+      } else {
       float4 bb[4], bn[4];
 #pragma unroll
       for (int j = 0; j < 3; ++j) bb[j] = Bp[(3 * w + j) * 64];
@@ -351,6 +473,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #pragma unroll
           for (int j = 0; j < 4; ++j) bb[j] = bn[j];
         }
+      }
       }
       NRMS_STAMP(3)
       prefetch_qk(nbuf);
@@ -393,10 +516,23 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           const int u = lane + 64 * u0;   // float4 column of the 300-d output
           if (u < FD / 4) {
             const float* src = ctxL + FL * t * SC + 4 * u;
+            const __bf16* srcb = ctxB + FL * t * XRB + 4 * u;
             float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
             for (int i = 0; i < FL; ++i) {
-              const float4 cv = *reinterpret_cast<const float4*>(src + i * SC);
+              float4 cv;
+              if constexpr (X6) {
+                // hi + mid + lo reconstructs the fp32 context exactly
+                const bf16x4 vh = *reinterpret_cast<const bf16x4*>(srcb + i * XRB);
+                const bf16x4 vm = *reinterpret_cast<const bf16x4*>(srcb + i * XRB + XKP);
+                const bf16x4 vl = *reinterpret_cast<const bf16x4*>(srcb + i * XRB + 2 * XKP);
+                cv = make_float4(((float)vh[0] + (float)vm[0]) + (float)vl[0],
+                                 ((float)vh[1] + (float)vm[1]) + (float)vl[1],
+                                 ((float)vh[2] + (float)vm[2]) + (float)vl[2],
+                                 ((float)vh[3] + (float)vm[3]) + (float)vl[3]);
+              } else {
+                cv = *reinterpret_cast<const float4*>(src + i * SC);
+              }
               acc.x = fmaf(wts[i], cv.x, acc.x);
               acc.y = fmaf(wts[i], cv.y, acc.y);
               acc.z = fmaf(wts[i], cv.z, acc.z);
@@ -418,14 +554,14 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 
 }  // namespace
 
-size_t fused_news_packed_b_floats() { return (size_t)WAP_FLOATS + SPECIAL_FLOATS; }
+size_t fused_news_packed_b_floats() { return (size_t)WAP_MAX + SPECIAL_FLOATS; }
 
 bool fused_news_supported(int L, int D, int H, int Q) {
   return L == FL && D == FD && H == FH && Q == FQ;
 }
 
 #ifdef NRMS_FUSED_TIMING
-unsigned long long* g_fused_dbg = nullptr;   // set by profiles/probes/fused_timing.hip
+unsigned long long* g_fused_dbg = nullptr;   // set by profiles/probes/news_variants.hip
 #define NRMS_TIMING_ARG , g_fused_dbg
 #else
 #define NRMS_TIMING_ARG
@@ -437,15 +573,22 @@ int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a
                           float* out, hipStream_t s) {
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16) return NRMS_ERR_UNSUPPORTED;
-  auto kern = &fused_news_kernel;
-  static bool attr_done = false;
-  if (!attr_done) {
+  const bool x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6;
+  auto kern = x6 ? &fused_news_kernel<true> : &fused_news_kernel<false>;
+  const size_t lds_bytes = x6 ? LDS_BYTES_X6 : LDS_BYTES;
+  static bool attr_done[2] = {false, false};
+  if (!attr_done[x6]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)LDS_BYTES);
-    attr_done = true;
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
+    attr_done[x6] = true;
   }
-  const int npk = WAP_FLOATS + SPECIAL_FLOATS;
-  hipLaunchKernelGGL(pack_additive_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap);
+  if (x6) {
+    const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
+    hipLaunchKernelGGL(pack_additive_b3_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap);
+  } else {
+    const int npk = WAP_FLOATS + SPECIAL_FLOATS;
+    hipLaunchKernelGGL(pack_additive_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap);
+  }
   if (int32_t st = launch_status()) return st;
   const int64_t n_groups = (n_titles + FT - 1) / FT;
   int dev = 0, n_cu = 256;
@@ -456,7 +599,7 @@ int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a
   }
   const int64_t blocks = n_groups < n_cu ? n_groups : n_cu;   // persistent: one workgroup per CU
   RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows};
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), LDS_BYTES, s, qkv, rm, n_groups,
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, rm, n_groups,
                      wap, b_add, q_add, out NRMS_TIMING_ARG);
   return launch_status();
 }

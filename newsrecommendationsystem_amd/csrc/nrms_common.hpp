@@ -65,6 +65,9 @@ struct WeightRows {
   int nseg;
 };
 
+// Process-wide GEMM arithmetic (nrms_set_gemm_arith; defined in capi.hip).
+int gemm_arith();
+
 // Host-side launchers (defined in the .hip files).
 int32_t launch_gather(const int64_t* ids, int64_t n_tok, const float* table, int64_t V, int D,
                       float* out, hipStream_t s);

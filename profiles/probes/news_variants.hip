@@ -1,0 +1,130 @@
+// Fused news kernel, both additive-GEMM variants (split-bf16 x6 and exact f32
+// MFMA) on the bench shape (56,320 titles, folded q|k|v table of V = 70,976
+// rows): wall time per launch (HIP events), output agreement between the
+// variants, and the per-phase shader-cycle breakdown (s_memtime stamps
+// compiled in with NRMS_FUSED_TIMING; a diagnostic build, the stamps cost time).
+//   hipcc -O3 --offload-arch=gfx950 -std=c++17 -I include \
+//     profiles/probes/news_variants.hip -o profiles/probes/news_variants
+//   ./news_variants [n_titles] [reps] [id_range]
+#ifndef NRMS_NO_STAMPS
+#define NRMS_FUSED_TIMING 1
+#endif
+#include "../../newsrecommendationsystem_amd/csrc/news_fused.hip"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+namespace nrms {
+void set_last_hip_error(hipError_t) {}
+int g_arith = NRMS_GEMM_SPLIT_BF16X6;
+int gemm_arith() { return g_arith; }
+}
+
+#define CK(x)                                                              \
+  do {                                                                     \
+    hipError_t e_ = (x);                                                   \
+    if (e_ != hipSuccess) {                                                \
+      printf("HIP error %s at %d\n", hipGetErrorString(e_), __LINE__);     \
+      return 1;                                                            \
+    }                                                                      \
+  } while (0)
+
+int main(int argc, char** argv) {
+  const int64_t V = 70976, n_titles = argc > 1 ? atoll(argv[1]) : 56320;
+  const int reps = argc > 2 ? atoi(argv[2]) : 5;
+  const int64_t id_range = argc > 3 ? atoll(argv[3]) : V - 2;   // small: the table slice stays in L2
+  std::vector<float> h_qkv((size_t)V * 900), h_wa(200 * 300), h_b(200), h_q(200);
+  std::vector<int64_t> h_ids((size_t)n_titles * 20);
+  uint64_t st = 12345;
+  auto rnd = [&]() { st = st * 6364136223846793005ULL + 1442695040888963407ULL; return (float)((st >> 40) & 0xFFFFFF) / 16777216.f; };
+  for (auto& v : h_qkv) v = (rnd() - 0.5f) * 1.5f;
+  for (auto& v : h_wa) v = (rnd() - 0.5f) * 0.1f;
+  for (auto& v : h_b) v = (rnd() - 0.5f) * 0.1f;
+  for (auto& v : h_q) v = (rnd() - 0.5f) * 0.2f;
+  for (size_t i = 0; i < h_ids.size(); ++i) h_ids[i] = 1 + (int64_t)(rnd() * id_range);
+  // a few padding tokens / an all-padding title, as the synthetic generator has
+  for (int t = 0; t < 20; ++t) h_ids[7 * 20 + t] = 0;
+  float *qkv, *wa, *b, *q, *wap, *out0, *out1;
+  int64_t* ids;
+  unsigned long long* dbg;
+  CK(hipMalloc(&qkv, h_qkv.size() * 4));
+  CK(hipMalloc(&wa, h_wa.size() * 4));
+  CK(hipMalloc(&b, 800));
+  CK(hipMalloc(&q, 800));
+  CK(hipMalloc(&wap, nrms::fused_news_packed_b_floats() * 4));
+  CK(hipMalloc(&out0, (size_t)n_titles * 300 * 4));
+  CK(hipMalloc(&out1, (size_t)n_titles * 300 * 4));
+  CK(hipMalloc(&ids, h_ids.size() * 8));
+  CK(hipMalloc(&dbg, 256 * 8 * 8 * 8));
+  CK(hipMemcpy(qkv, h_qkv.data(), h_qkv.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(wa, h_wa.data(), h_wa.size() * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(b, h_b.data(), 800, hipMemcpyHostToDevice));
+  CK(hipMemcpy(q, h_q.data(), 800, hipMemcpyHostToDevice));
+  CK(hipMemcpy(ids, h_ids.data(), h_ids.size() * 8, hipMemcpyHostToDevice));
+#ifdef NRMS_FUSED_TIMING
+  nrms::g_fused_dbg = dbg;
+#endif
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const char* vname[2] = {"exact f32 MFMA", "split-bf16 x6"};
+  const int nwaves[2] = {4, 4};
+  for (int var = 1; var >= 0; --var) {
+    nrms::g_arith = var ? NRMS_GEMM_SPLIT_BF16X6 : NRMS_GEMM_F32;
+    float* out = var ? out1 : out0;
+    for (int it = 0; it < 2; ++it)
+      if (nrms::launch_fused_news(qkv, V, ids, n_titles, nullptr, n_titles, wa, b, q, wap, out, 0)) return 2;
+    CK(hipDeviceSynchronize());
+    CK(hipMemset(dbg, 0, 256 * 8 * 8 * 8));
+    CK(hipEventRecord(e0, 0));
+    for (int it = 0; it < reps; ++it)
+      if (nrms::launch_fused_news(qkv, V, ids, n_titles, nullptr, n_titles, wa, b, q, wap, out, 0)) return 2;
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("%s: kernel avg %.4f ms (pack + fused), %lld titles\n", vname[var], ms / reps, (long long)n_titles);
+#ifdef NRMS_FUSED_TIMING
+    std::vector<unsigned long long> h_dbg(256 * 8 * 8);
+    CK(hipMemcpy(h_dbg.data(), dbg, h_dbg.size() * 8, hipMemcpyDeviceToHost));
+    const char* names[7] = {"barrier0", "A", "barrier1", "B main", "B epi", "barrier2", "C"};
+    const int nk = 7;
+    for (int w = 0; w < nwaves[var]; ++w) {
+      printf("  wave %d:", w);
+      double tot = 0;
+      for (int k = 0; k < nk; ++k) {
+        double s = 0;
+        // the last launch only (dbg is overwritten per launch)
+        for (int blk = 0; blk < 256; ++blk) s += h_dbg[(blk * nwaves[var] + w) * 8 + k];
+        s /= 256;
+        tot += s;
+        printf(" %s=%.0f", names[k], s);
+      }
+      printf(" | total=%.0f\n", tot);
+    }
+#endif
+  }
+  std::vector<float> a((size_t)n_titles * 300), c((size_t)n_titles * 300);
+  CK(hipMemcpy(a.data(), out0, a.size() * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(c.data(), out1, c.size() * 4, hipMemcpyDeviceToHost));
+  double worst = 0, num = 0, den = 0;
+  size_t nan_mismatch = 0;
+  for (int64_t t = 0; t < n_titles; ++t) {
+    double n2 = 0, d2 = 0;
+    for (int d = 0; d < 300; ++d) {
+      const float x = a[t * 300 + d], y = c[t * 300 + d];
+      if (std::isnan(x) != std::isnan(y)) ++nan_mismatch;
+      if (std::isnan(x) || std::isnan(y)) continue;
+      n2 += (double)(x - y) * (x - y);
+      d2 += (double)y * y;
+    }
+    num += n2; den += d2;
+    const double r = d2 > 0 ? std::sqrt(n2 / d2) : std::sqrt(n2);
+    if (r > worst) worst = r;
+  }
+  printf("x6 vs f32: max normwise rel err %.3e, overall %.3e, NaN mismatches %zu\n", worst,
+         std::sqrt(num / den), nan_mismatch);
+  return (worst < 2e-6 && nan_mismatch == 0) ? 0 : 3;
+}

@@ -33,3 +33,13 @@ def device():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=["x6", "f32"])
+def gemm_mode(request):
+    """Run a GPU test under both GEMM arithmetics (include/nrms_hip.h,
+    nrms_set_gemm_arith): split-bf16 x6 (default) and exact f32 MFMA."""
+    from newsrecommendationsystem_amd import _native as N
+    mode = N.NRMS_GEMM_SPLIT_BF16X6 if request.param == "x6" else N.NRMS_GEMM_F32
+    with N.gemm_arith(mode):
+        yield request.param

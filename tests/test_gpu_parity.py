@@ -82,7 +82,7 @@ def test_gather_bad_id_is_nan_not_fault(device):
 
 
 @pytest.mark.parametrize("mode", [1, 2, "cached"])
-def test_news_vectors_golden(golden, golden_state, device, mode):
+def test_news_vectors_golden(golden, golden_state, device, mode, gemm_mode):
     knobs = {"hip_cache_folded_table": mode == "cached"}
     if mode != "cached":
         knobs["hip_proj_mode"] = mode
@@ -93,7 +93,7 @@ def test_news_vectors_golden(golden, golden_state, device, mode):
     assert err.max() < TOL, err.max()
 
 
-def test_user_vectors_golden(golden, gold_model):
+def test_user_vectors_golden(golden, gold_model, gemm_mode):
     u_in = W.normal(int(golden["seed"]), 30, (8, 50, 300), 0.3)
     for b, n in enumerate(golden["user_len"]):
         u_in[b, : 50 - n] = 0.0
@@ -115,7 +115,7 @@ def test_user_vectors_noncontiguous_input(golden, gold_model, device):
 
 
 @pytest.mark.parametrize("mode", [0, 1, 2])
-def test_forward_golden(golden, golden_state, device, mode):
+def test_forward_golden(golden, golden_state, device, mode, gemm_mode):
     m = _module(golden_state, int(golden["V"]), device, hip_proj_mode=mode)
     cand = golden["fwd_cand"].astype(np.int64)
     clk = golden["fwd_clicked"].astype(np.int64)
@@ -137,7 +137,7 @@ def test_prediction_golden(golden, gold_model, device):
     assert np.abs(out - golden["pred_out"]).max() <= 1e-4 * np.abs(golden["pred_out"]).max()
 
 
-def test_raw_exp_overflow_nan(golden, golden_state, device):
+def test_raw_exp_overflow_nan(golden, golden_state, device, gemm_mode):
     sd = dict(golden_state)
     for k in ("W_Q", "W_K"):
         key = f"news_encoder.multihead_self_attention.{k}.weight"
@@ -156,7 +156,7 @@ def test_raw_exp_overflow_nan(golden, golden_state, device):
         assert O.normwise_rel_err(out[~nan_ref], ref[~nan_ref]).max() < TOL
 
 
-def test_raw_exp_underflow_zero(golden, golden_state, device):
+def test_raw_exp_underflow_zero(golden, golden_state, device, gemm_mode):
     sd = dict(golden_state)
     pre = "news_encoder.multihead_self_attention"
     b = golden["underflow_bias"]
@@ -210,7 +210,7 @@ def test_empty_batch(gold_model):
 
 
 @pytest.mark.parametrize("B,C,N", [(1, 1, 1), (3, 5, 50), (37, 5, 50), (5, 2, 7)])
-def test_forward_shapes_vs_oracle(device, B, C, N):
+def test_forward_shapes_vs_oracle(device, B, C, N, gemm_mode):
     V = 4096
     sd = W.nrms_state(11, V)
     m = _module(sd, V, device)
@@ -238,7 +238,7 @@ def test_full_vocab_forward_vs_oracle(device):
 
 
 @pytest.mark.parametrize("n", [1, 3, 4, 5, 4099])
-def test_fused_news_tail_vs_stages(device, n):
+def test_fused_news_tail_vs_stages(device, n, gemm_mode):
     """Fused tail == separate stage kernels (within fp32 reordering), including
     partial last blocks (n % 4 != 0), through both id arrays."""
     from newsrecommendationsystem_amd import _native as N
@@ -270,7 +270,7 @@ def test_fused_news_tail_vs_stages(device, n):
     assert O.normwise_rel_err(_np(out), oracle).max() < TOL
 
 
-def test_full_size_properties(device):
+def test_full_size_properties(device, gemm_mode):
     """BASELINE config 3 (B = 1024, 1+K = 5, 50 clicked, V = 70,976): size-
     independent properties — folded == direct within fp32 rounding, sharding
     the batch changes nothing (each impression depends only on its own rows),
@@ -335,7 +335,7 @@ def test_stage_abi_matches_module(golden, golden_state, device):
 
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("mode", [1, 2])
-def test_plan_matches_forward(device, fused, mode):
+def test_plan_matches_forward(device, fused, mode, gemm_mode):
     """pipeline.ForwardPlan (stage calls, as timed by bench.py) == nrms_forward."""
     from newsrecommendationsystem_amd.pipeline import ForwardPlan
     V = 3000
@@ -352,3 +352,27 @@ def test_plan_matches_forward(device, fused, mode):
     else:
         assert ((y - ref).norm() / ref.norm()) < 1e-5
     assert np.abs(_np(y) - O.forward(cand, clk, sd, np.float64)).max() <= TOL * np.abs(_np(y)).max()
+
+
+def test_split_bf16x6_accuracy_matches_f32(device):
+    """The split-bf16 x6 GEMMs are as accurate as the exact-f32 MFMA GEMMs:
+    against the fp64 oracle, the x6 forward's error is within 2x the f32
+    forward's (both ~1e-7 normwise), on the full vocabulary."""
+    from newsrecommendationsystem_amd import _native as N
+    V = 70976
+    sd = W.nrms_state(17, V)
+    m = _module(sd, V, device, hip_cache_folded_table=False)
+    cand, clk, _ = W.impressions(17, 77, 24, V)
+    ref = O.forward(cand, clk, sd, np.float64)
+    news_ids = W.titles(17, 78, 64, V, min_len=1)
+    nref = O.news_encode(news_ids, sd, np.float64)
+    errs = {}
+    for mode in (N.NRMS_GEMM_SPLIT_BF16X6, N.NRMS_GEMM_F32):
+        with N.gemm_arith(mode), torch.no_grad():
+            y = _np(m.forward_ids(torch.from_numpy(cand), torch.from_numpy(clk)))
+            nv = _np(m.get_news_vector({"title": torch.from_numpy(news_ids)}))
+        errs[mode] = (O.normwise_rel_err(y.reshape(1, -1), ref.reshape(1, -1)).max(),
+                      O.normwise_rel_err(nv, nref).max())
+    x6, f32 = errs[N.NRMS_GEMM_SPLIT_BF16X6], errs[N.NRMS_GEMM_F32]
+    assert x6[0] < 1e-5 and x6[1] < 1e-5, errs
+    assert x6[0] <= 2 * f32[0] + 1e-7 and x6[1] <= 2 * f32[1] + 1e-7, errs

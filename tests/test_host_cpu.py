@@ -57,6 +57,20 @@ def test_exports_every_declared_symbol():
     assert set(declared) == set(N.SIGNATURES), set(declared) ^ set(N.SIGNATURES)
 
 
+def test_gemm_arith_setting_without_gpu():
+    """Process-wide GEMM arithmetic: default split-bf16x6 (unless NRMS_GEMM=f32),
+    settable, unknown modes rejected without changing the setting."""
+    from newsrecommendationsystem_amd import _native as N
+    lib = N.load()
+    start = lib.nrms_get_gemm_arith()
+    assert start in (N.NRMS_GEMM_SPLIT_BF16X6, N.NRMS_GEMM_F32)
+    with N.gemm_arith(N.NRMS_GEMM_F32):
+        assert lib.nrms_get_gemm_arith() == N.NRMS_GEMM_F32
+        assert lib.nrms_set_gemm_arith(7) < 0
+        assert lib.nrms_get_gemm_arith() == N.NRMS_GEMM_F32
+    assert lib.nrms_get_gemm_arith() == start
+
+
 def test_abi_queries_without_gpu():
     from newsrecommendationsystem_amd import _native as N
     lib = N.load()
