@@ -22,7 +22,8 @@
  *     mirroring nn.Embedding's IndexError). An out-of-range id never reads out
  *     of bounds: its row is produced as NaN.
  *   - Eval-mode semantics (dropout = identity, src/model/NRMS/news_encoder.py:
- *     38-40,43-45). Training kernels are not part of this ABI version.
+ *     38-40,43-45) for the scoring path; the training kernels at the end of
+ *     this header provide the train-mode forward pieces and the backward.
  */
 #ifndef NRMS_HIP_H
 #define NRMS_HIP_H
@@ -200,6 +201,73 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
                      const nrms_encoder_weights_t* news_w, const nrms_encoder_weights_t* user_w,
                      int32_t proj_mode, float* logits, void* workspace, size_t workspace_bytes,
                      hipStream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Training kernels: the train-mode forward pieces and the backward of the path
+ * above, as src/train.py:202-236 needs them (loss.backward(), Adam step). The
+ * Python glue (newsrecommendationsystem_amd/train_hip.py) chains them in a
+ * torch.autograd.Function. Gradient outputs named d_* are ACCUMULATED into
+ * (callers zero them), dx / dqkv / dnews outputs are overwritten. fp32; the
+ * GEMMs of the backward use f32 MFMA whatever nrms_set_gemm_arith says. */
+
+/* F.dropout(x, p, training=True) (news_encoder.py:38-40,43-45): y[i] = x[i] /
+ * (1-p) if u(seed, i) >= p else 0, u a counter-based uniform (splitmix64 of
+ * seed and i), so the same call on the gradient is the backward. 0 <= p < 1;
+ * x == y allowed. */
+int32_t nrms_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed,
+                     hipStream_t stream);
+
+/* AdditiveAttention.forward (additive.py:27-53) keeping what the backward
+ * needs: y_tanh[n_seq*L, Q] = tanh(x W^T + b), scores[n_seq*L] = y . q,
+ * out[n_seq, D] = sum_l softmax_l(scores) x_l. */
+int32_t nrms_additive_forward_train(const float* x, int64_t n_seq, int32_t L,
+                                    const nrms_encoder_weights_t* w, float* y_tanh, float* scores,
+                                    float* out, hipStream_t stream);
+
+/* Its backward: dx[n_seq*L, D] (written) from dout[n_seq, D]; d_w_add [Q, D],
+ * d_b_add [Q], d_q_add [Q] accumulated. Workspace:
+ * nrms_additive_backward_workspace_size bytes. */
+size_t nrms_additive_backward_workspace_size(int64_t n_seq, int32_t L, int32_t D, int32_t Q);
+int32_t nrms_additive_backward(const float* x, int64_t n_seq, int32_t L,
+                               const nrms_encoder_weights_t* w, const float* y_tanh,
+                               const float* scores, const float* dout, float* dx, float* d_w_add,
+                               float* d_b_add, float* d_q_add, void* workspace,
+                               size_t workspace_bytes, hipStream_t stream);
+
+/* Backward of nrms_self_attention over per-token rows (row s*L + i of
+ * qkv[n_seq*L, 3D]): dqkv[n_seq*L, 3D] (written) from dctx[n_seq*L, D],
+ * recomputing the raw-exp attention (multihead_self.py:15-23). L <= 64. */
+int32_t nrms_self_attention_backward(const float* qkv, const float* dctx, int64_t n_seq,
+                                     int32_t L, const nrms_encoder_weights_t* w, float* dqkv,
+                                     hipStream_t stream);
+
+/* Backward of nrms_qkv_project (identity rows): dx[rows, D] = dqkv [W_Q; W_K;
+ * W_V] (written; NULL skips it), d_w_qkv[3D, D] += dqkv^T x, d_b_qkv[3D] +=
+ * column sums of dqkv. Workspace: nrms_qkv_project_backward_workspace_size. */
+size_t nrms_qkv_project_backward_workspace_size(int32_t D);
+int32_t nrms_qkv_project_backward(const float* x, int64_t rows, const nrms_encoder_weights_t* w,
+                                  const float* dqkv, float* dx, float* d_w_qkv, float* d_b_qkv,
+                                  void* workspace, size_t workspace_bytes, hipStream_t stream);
+
+/* Backward of nrms_score (dot_product.py:8-19): dnews[B, C, D] (contiguous,
+ * written) = dlogits[b, c] user[b]; duser[B, D] (written) = sum_c dlogits[b, c]
+ * news[b, c]. Strides as nrms_score. */
+int32_t nrms_score_backward(const float* news, int64_t B, int32_t C, int64_t stride_b,
+                            int64_t stride_c, const float* user, int64_t stride_u, int32_t D,
+                            const float* dlogits, float* dnews, float* duser, hipStream_t stream);
+
+/* Backward of nrms_embedding_gather as nn.Embedding(padding_idx) computes it:
+ * dtable[ids[t]] += dx[t] for every t with ids[t] != padding_idx (dense
+ * [V, D] gradient, accumulated). */
+int32_t nrms_embedding_backward(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
+                                int32_t D, int64_t padding_idx, float* dtable,
+                                hipStream_t stream);
+
+/* torch.optim.Adam step (src/train.py:127; amsgrad off, no weight decay) on
+ * one parameter, in torch's operation order; `step` counts from 1. */
+int32_t nrms_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                       int64_t n, float lr, float beta1, float beta2, float eps, int64_t step,
+                       hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -57,6 +57,18 @@ SIGNATURES = {
     "nrms_score": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p]),
     "nrms_score_pairs": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _i32, _p, _p]),
     "nrms_impression_metrics": (_i32, [_p, _p, _p, _i64, _p, _p]),
+    # training kernels
+    "nrms_dropout": (_i32, [_p, _p, _i64, ctypes.c_float, ctypes.c_uint64, _p]),
+    "nrms_additive_forward_train": (_i32, [_p, _i64, _i32, _EW, _p, _p, _p, _p]),
+    "nrms_additive_backward_workspace_size": (_sz, [_i64, _i32, _i32, _i32]),
+    "nrms_additive_backward": (_i32, [_p, _i64, _i32, _EW, _p, _p, _p, _p, _p, _p, _p, _p, _sz, _p]),
+    "nrms_self_attention_backward": (_i32, [_p, _p, _i64, _i32, _EW, _p, _p]),
+    "nrms_qkv_project_backward_workspace_size": (_sz, [_i32]),
+    "nrms_qkv_project_backward": (_i32, [_p, _i64, _EW, _p, _p, _p, _p, _p, _sz, _p]),
+    "nrms_score_backward": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p, _p, _p]),
+    "nrms_embedding_backward": (_i32, [_p, _i64, _p, _i64, _i32, _i64, _p, _p]),
+    "nrms_adam_step": (_i32, [_p, _p, _p, _p, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                              ctypes.c_float, _i64, _p]),
     "nrms_forward_workspace_size": (_sz, [_i64, _i32, _i32, _i32, _i64, _i32, _i32]),
     "nrms_forward": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _p, _i64, _EW, _EW, _i32, _p, _p,
                             _sz, _p]),

@@ -376,4 +376,133 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
                       stream);
 }
 
+
+// ---------------------------------------------------------------------------
+// Training kernels (train-mode forward pieces, backward, optimizer step).
+
+int32_t nrms_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed,
+                     hipStream_t stream) {
+  if (n < 0 || !(p >= 0.f && p < 1.f)) return NRMS_ERR_INVALID_ARG;
+  if (n > 0 && (!x || !y)) return NRMS_ERR_INVALID_ARG;
+  return launch_dropout(x, y, n, p, seed, stream);
+}
+
+int32_t nrms_additive_forward_train(const float* x, int64_t n_seq, int32_t L,
+                                    const nrms_encoder_weights_t* w, float* y_tanh, float* scores,
+                                    float* out, hipStream_t stream) {
+  if (n_seq < 0 || L <= 0) return NRMS_ERR_INVALID_ARG;
+  if (!weights_ok(w)) return NRMS_ERR_INVALID_ARG;
+  if (n_seq == 0) return NRMS_OK;
+  if (!x || !y_tanh || !scores || !out) return NRMS_ERR_INVALID_ARG;
+  int32_t st = launch_gemm_additive_score_y(x, n_seq * L, w->d_model, w->w_add, w->b_add, w->q_add,
+                                            w->query_dim, scores, y_tanh, stream);
+  if (st) return st;
+  return launch_additive_pool(x, scores, n_seq, L, w->d_model, out, stream);
+}
+
+size_t nrms_additive_backward_workspace_size(int64_t n_seq, int32_t L, int32_t D, int32_t Q) {
+  if (n_seq < 0 || L <= 0 || D <= 0 || Q <= 0) return 0;
+  return align_up((size_t)n_seq * L * Q * 4) + align_up((size_t)D * Q * 4);
+}
+
+int32_t nrms_additive_backward(const float* x, int64_t n_seq, int32_t L,
+                               const nrms_encoder_weights_t* w, const float* y_tanh,
+                               const float* scores, const float* dout, float* dx, float* d_w_add,
+                               float* d_b_add, float* d_q_add, void* workspace,
+                               size_t workspace_bytes, hipStream_t stream) {
+  if (n_seq < 0 || L <= 0) return NRMS_ERR_INVALID_ARG;
+  if (!weights_ok(w)) return NRMS_ERR_INVALID_ARG;
+  if (n_seq == 0) return NRMS_OK;
+  if (!x || !y_tanh || !scores || !dout || !dx || !d_w_add || !d_b_add || !d_q_add)
+    return NRMS_ERR_INVALID_ARG;
+  const int D = w->d_model, Q = w->query_dim;
+  if (D % 4 != 0 || Q % 4 != 0) return NRMS_ERR_UNSUPPORTED;
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* dz = cv.floats((size_t)n_seq * L * Q);
+  float* waT = cv.floats((size_t)D * Q);
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  int32_t st = launch_additive_backward_rows(x, y_tanh, scores, w->q_add, dout, n_seq, L, D, Q, dx,
+                                             dz, d_q_add, d_b_add, stream);
+  if (st) return st;
+  const float* wa[1] = {w->w_add};
+  st = launch_transpose(wa, 1, Q, D, waT, stream);   // [Q, D] -> [D, Q]
+  if (st) return st;
+  WeightRows r{};
+  r.w[0] = waT;
+  r.b[0] = nullptr;
+  r.seg_rows = D;
+  r.nseg = 1;
+  r.accumulate = 1;
+  st = launch_gemm_store_f32(dz, n_seq * L, Q, r, D, dx, D, stream);   // dx += dz W_add
+  if (st) return st;
+  return launch_gemm_tn(dz, n_seq * L, Q, x, D, d_w_add, nullptr, stream);   // dW += dz^T x
+}
+
+int32_t nrms_self_attention_backward(const float* qkv, const float* dctx, int64_t n_seq,
+                                     int32_t L, const nrms_encoder_weights_t* w, float* dqkv,
+                                     hipStream_t stream) {
+  if (n_seq < 0 || L <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (n_seq == 0) return NRMS_OK;
+  if (!qkv || !dctx || !dqkv) return NRMS_ERR_INVALID_ARG;
+  return launch_mhsa_backward(qkv, dctx, n_seq, L, w->d_model, w->n_heads, dqkv, stream);
+}
+
+size_t nrms_qkv_project_backward_workspace_size(int32_t D) {
+  if (D <= 0) return 0;
+  return align_up((size_t)3 * D * D * 4);
+}
+
+int32_t nrms_qkv_project_backward(const float* x, int64_t rows, const nrms_encoder_weights_t* w,
+                                  const float* dqkv, float* dx, float* d_w_qkv, float* d_b_qkv,
+                                  void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  if (rows < 0) return NRMS_ERR_INVALID_ARG;
+  if (!weights_ok(w)) return NRMS_ERR_INVALID_ARG;
+  if (rows == 0) return NRMS_OK;
+  if (!x || !dqkv || !d_w_qkv || !d_b_qkv) return NRMS_ERR_INVALID_ARG;
+  const int D = w->d_model;
+  int32_t st;
+  if (dx) {
+    Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+    float* wT = cv.floats((size_t)3 * D * D);
+    if (!cv.ok) return NRMS_ERR_WORKSPACE;
+    const float* ws3[3] = {w->w_q, w->w_k, w->w_v};
+    st = launch_transpose(ws3, 3, D, D, wT, stream);   // [3D, D] -> [D, 3D]
+    if (st) return st;
+    WeightRows r{};
+    r.w[0] = wT;
+    r.b[0] = nullptr;
+    r.seg_rows = D;
+    r.nseg = 1;
+    st = launch_gemm_store_f32(dqkv, rows, 3 * D, r, D, dx, D, stream);   // dx = dqkv [Wq; Wk; Wv]
+    if (st) return st;
+  }
+  return launch_gemm_tn(dqkv, rows, 3 * D, x, D, d_w_qkv, d_b_qkv, stream);
+}
+
+int32_t nrms_score_backward(const float* news, int64_t B, int32_t C, int64_t stride_b,
+                            int64_t stride_c, const float* user, int64_t stride_u, int32_t D,
+                            const float* dlogits, float* dnews, float* duser, hipStream_t stream) {
+  if (B < 0 || C < 0 || D <= 0) return NRMS_ERR_INVALID_ARG;
+  if (B * C > 0 && (!news || !user || !dlogits || !dnews || !duser)) return NRMS_ERR_INVALID_ARG;
+  return launch_score_backward(news, B, C, stride_b, stride_c, user, stride_u, D, dlogits, dnews,
+                               duser, stream);
+}
+
+int32_t nrms_embedding_backward(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
+                                int32_t D, int64_t padding_idx, float* dtable,
+                                hipStream_t stream) {
+  if (n_tok < 0 || V <= 0 || D <= 0) return NRMS_ERR_INVALID_ARG;
+  if (n_tok > 0 && (!ids || !dx || !dtable)) return NRMS_ERR_INVALID_ARG;
+  return launch_embedding_backward(ids, n_tok, dx, V, D, padding_idx, dtable, stream);
+}
+
+int32_t nrms_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,
+                       int64_t n, float lr, float beta1, float beta2, float eps, int64_t step,
+                       hipStream_t stream) {
+  if (n < 0 || step < 1) return NRMS_ERR_INVALID_ARG;
+  if (n > 0 && (!param || !grad || !exp_avg || !exp_avg_sq)) return NRMS_ERR_INVALID_ARG;
+  return launch_adam(param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, step, stream);
+}
+
 }  // extern "C"

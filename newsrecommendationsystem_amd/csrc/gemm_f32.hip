@@ -147,13 +147,16 @@ __device__ __forceinline__ void gemm_tile(
       const int col = n0 + tn * 16 + lm;
       if (col >= N) continue;
       const int seg = col / wr.seg_rows;
-      const float bias = wr.b[seg][col - seg * wr.seg_rows];
+      const float bias = wr.b[seg] ? wr.b[seg][col - seg * wr.seg_rows] : 0.f;
 #pragma unroll
       for (int ms = 0; ms < 2; ++ms)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int64_t row = row_base + ms * 16 + r;
-          if (row < M) Y[row * ldy + col] = acc[ms][tn][r] + bias;
+          if (row < M) {
+            float* yp = Y + row * ldy + col;
+            *yp = (wr.accumulate ? *yp : 0.f) + acc[ms][tn][r] + bias;
+          }
         }
     }
   } else {
@@ -169,9 +172,14 @@ __device__ __forceinline__ void gemm_tile(
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float part = 0.f;
+        const int64_t yrow = row_base + ms * 16 + r;
 #pragma unroll
         for (int tn = 0; tn < TN; ++tn)
-          if (tn * 16 + lm < N) part = fmaf(qv[tn], tanhf(acc[ms][tn][r] + bv[tn]), part);
+          if (tn * 16 + lm < N) {
+            const float t = tanhf(acc[ms][tn][r] + bv[tn]);
+            if (Y && yrow < M) Y[yrow * N + tn * 16 + lm] = t;   // training forward keeps y
+            part = fmaf(qv[tn], t, part);
+          }
         part += __shfl_xor(part, 1);
         part += __shfl_xor(part, 2);
         part += __shfl_xor(part, 4);
@@ -441,9 +449,30 @@ int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_i
   return launch_status();
 }
 
+int32_t launch_gemm_store_f32(const float* X, int64_t M, int K, const WeightRows& w, int N, float* Y,
+                              int64_t ldy, hipStream_t s) {
+  if (M == 0) return NRMS_OK;
+  if (K % 4 != 0 || ((uintptr_t)X % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  for (int i = 0; i < w.nseg; ++i)
+    if (((uintptr_t)w.w[i] % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  const int nct = (N + 16 * TN_STORE - 1) / (16 * TN_STORE);
+  const int64_t blocks = (M + BM - 1) / BM * nct;
+  if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, TN_STORE, false>), dim3((unsigned)blocks),
+                     dim3(kThreads), 0, s, X, M, (const int64_t*)nullptr, M, K, w, N, Y, ldy,
+                     (const float*)nullptr, (float*)nullptr, nct);
+  return launch_status();
+}
+
 int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
                                    const float* b, const float* q, int N, float* score,
                                    hipStream_t s) {
+  return launch_gemm_additive_score_y(X, M, K, W, b, q, N, score, nullptr, s);
+}
+
+int32_t launch_gemm_additive_score_y(const float* X, int64_t M, int K, const float* W,
+                                     const float* b, const float* q, int N, float* score,
+                                     float* y_out, hipStream_t s) {
   if (M == 0) return NRMS_OK;
   if (N > 16 * TN_ADDITIVE) return NRMS_ERR_UNSUPPORTED;
   if (K % 4 != 0 || ((uintptr_t)X % 16) != 0 || ((uintptr_t)W % 16) != 0)
@@ -457,7 +486,7 @@ int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float
   if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_ADDITIVE, TN_ADDITIVE, true>), dim3((unsigned)blocks),
                      dim3(kThreads), 0, s, X, M, (const int64_t*)nullptr, M, K, w, N,
-                     (float*)nullptr, (int64_t)0, q, score, 1);
+                     y_out, (int64_t)N, q, score, 1);
   return launch_status();
 }
 

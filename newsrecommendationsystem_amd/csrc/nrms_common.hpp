@@ -60,9 +60,10 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
 // (the Q|K|V projection is three nn.Linear weights used as one N = 3D GEMM).
 struct WeightRows {
   const float* w[3];
-  const float* b[3];
+  const float* b[3];   // may be null: no bias
   int seg_rows;
   int nseg;
+  int accumulate = 0;  // f32 store GEMM only: Y += X W^T (+ b)
 };
 
 // Process-wide GEMM arithmetic (nrms_set_gemm_arith; defined in capi.hip).
@@ -82,6 +83,33 @@ int32_t launch_mhsa(const float* qkv, int64_t n_rows, const int64_t* ids_a, int6
                     hipStream_t s);
 int32_t launch_additive_pool(const float* x, const float* score, int64_t n_seq, int L, int D,
                              float* out, hipStream_t s);
+// f32-MFMA store GEMM regardless of the process-wide arithmetic (training path).
+int32_t launch_gemm_store_f32(const float* X, int64_t M, int K, const WeightRows& w, int N, float* Y,
+                              int64_t ldy, hipStream_t s);
+// Additive projection GEMM that also stores y = tanh(X W^T + b) [M, N] (training forward).
+int32_t launch_gemm_additive_score_y(const float* X, int64_t M, int K, const float* W,
+                                     const float* b, const float* q, int N, float* score,
+                                     float* y_out, hipStream_t s);
+// training kernels (train.hip)
+int32_t launch_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, hipStream_t s);
+int32_t launch_score_backward(const float* news, int64_t B, int C, int64_t sb, int64_t sc,
+                              const float* user, int64_t su, int D, const float* dl, float* dnews,
+                              float* duser, hipStream_t s);
+int32_t launch_additive_backward_rows(const float* x, const float* y, const float* score,
+                                      const float* q, const float* dout, int64_t n_seq, int L,
+                                      int D, int Q, float* dx, float* dz, float* dq, float* db,
+                                      hipStream_t s);
+int32_t launch_mhsa_backward(const float* qkv, const float* dctx, int64_t n_seq, int L, int D,
+                             int H, float* dqkv, hipStream_t s);
+int32_t launch_gemm_tn(const float* dY, int64_t R, int N, const float* X, int K, float* dW,
+                       float* db, hipStream_t s);
+int32_t launch_transpose(const float* const* src, int nseg, int seg_rows, int cols, float* dst,
+                         hipStream_t s);
+int32_t launch_embedding_backward(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
+                                  int D, int64_t padding_idx, float* dtable, hipStream_t s);
+int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+                    float b2, float eps, int64_t step, hipStream_t s);
+
 size_t fused_news_packed_b_floats();
 bool fused_news_supported(int L, int D, int H, int Q);
 int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a,

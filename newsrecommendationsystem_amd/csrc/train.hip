@@ -1,0 +1,389 @@
+// Training (train-mode forward + backward + Adam) kernels of the NRMS path:
+// the autograd of src/model/NRMS (news_encoder.py:27-48, user_encoder.py:15-26,
+// multihead_self.py:15-75, additive.py:27-53, dot_product.py:8-19) and the
+// optimizer step of src/train.py:127,205-236, restated as explicit backward
+// kernels. fp32 throughout; the weight-gradient GEMM runs on f32 MFMA.
+//
+//   dropout            counter-based: keep(i) = hash(seed, i) >= p, so the
+//                      backward regenerates the mask instead of storing it
+//   score_backward     d news = dlogit * user, d user = sum_c dlogit * news
+//   additive_backward  softmax / tanh·q chain per sequence; dz = ds q (1 - y^2)
+//   mhsa_backward      raw-exp attention per (sequence, head): A = E / (Z + 1e-8),
+//                      dS = A (dA - rowsum(dA A)), dQ = dS K / sqrt(dk), ...
+//   gemm_tn            dW[n][k] += sum_r dY[r][n] X[r][k] (split over rows, atomics)
+//   embedding_backward dtable[id] += dx (rows with id == padding_idx skipped)
+//   adam               torch.optim.Adam's update, same operation order
+#include "nrms_common.hpp"
+
+namespace nrms {
+namespace {
+
+// splitmix64 finaliser of (seed, index): uniform in [0, 1) with 24 bits.
+__device__ __forceinline__ float uniform01(uint64_t seed, uint64_t i) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ULL * (i + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+
+__global__ __launch_bounds__(256) void dropout_kernel(const float* __restrict__ x,
+                                                      float* __restrict__ y, int64_t n, float p,
+                                                      float scale, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  y[i] = uniform01(seed, (uint64_t)i) >= p ? x[i] * scale : 0.f;
+}
+
+// One wave per (impression b): duser[b] = sum_c dl[b,c] news[b,c,:];
+// dnews[b,c,:] = dl[b,c] user[b,:] (dnews contiguous [B, C, D]).
+__global__ __launch_bounds__(256) void score_backward_kernel(
+    const float* __restrict__ news, int64_t B, int C, int64_t sb, int64_t sc,
+    const float* __restrict__ user, int64_t su, int D, const float* __restrict__ dl,
+    float* __restrict__ dnews, float* __restrict__ duser) {
+  const int lane = threadIdx.x & 63;
+  const int64_t b = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= B) return;
+  for (int d = lane; d < D; d += 64) {
+    const float u = user[b * su + d];
+    float acc = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float g = dl[b * C + c];
+      acc = fmaf(g, news[b * sb + c * sc + d], acc);
+      dnews[(b * C + c) * D + d] = g * u;
+    }
+    duser[b * D + d] = acc;
+  }
+}
+
+// Additive attention backward, per sequence s (one workgroup of 256 threads):
+//   w = softmax_l(score), out = sum_l w_l x_l
+//   dx_l   = w_l dout                    (written; the dz·Wa term is added by a GEMM)
+//   dw_l   = x_l · dout
+//   ds_l   = w_l (dw_l - sum_l' w_l' dw_l')
+//   dz_lq  = ds_l q_q (1 - y_lq^2)       (written, [rows, Q])
+//   dq    += sum_l ds_l y_l ;  db += sum_l dz_l   (atomics, one per column per sequence)
+__global__ __launch_bounds__(256) void additive_backward_rows_kernel(
+    const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ score,
+    const float* __restrict__ q, const float* __restrict__ dout, int L, int D, int Q,
+    float* __restrict__ dx, float* __restrict__ dz, float* __restrict__ dq,
+    float* __restrict__ db) {
+  __shared__ float sw[64], sds[64], sdw[64];
+  const int64_t s = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* xs = x + s * L * D;
+  const float* os = dout + s * D;
+  // dw_l = x_l . dout: wave wv takes rows wv, wv+4, ...
+  for (int l = wv; l < L; l += 4) {
+    float a = 0.f;
+    for (int d = lane; d < D; d += 64) a = fmaf(xs[l * D + d], os[d], a);
+    a = wave_sum(a);
+    if (lane == 0) sdw[l] = a;
+  }
+  __syncthreads();
+  if (wv == 0) {
+    const float v = lane < L ? score[s * L + lane] : -INFINITY;
+    const float m = wave_max_nan(v);
+    const float e = lane < L ? expf(v - m) : 0.f;
+    const float w = e / wave_sum(e);
+    const float dwv = lane < L ? sdw[lane] : 0.f;
+    const float dot = wave_sum(lane < L ? w * dwv : 0.f);
+    if (lane < L) {
+      sw[lane] = w;
+      sds[lane] = w * (dwv - dot);
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < L * D; e += 256) {
+    const int l = e / D, d = e - l * D;
+    dx[(s * L + l) * D + d] = sw[l] * os[d];
+  }
+  for (int qq = tid; qq < Q; qq += 256) {
+    const float qv = q[qq];
+    float aq = 0.f, ab = 0.f;
+    for (int l = 0; l < L; ++l) {
+      const float yv = y[(s * L + l) * Q + qq];
+      const float g = sds[l] * qv * (1.f - yv * yv);
+      dz[(s * L + l) * Q + qq] = g;
+      aq = fmaf(sds[l], yv, aq);
+      ab += g;
+    }
+    atomicAdd(dq + qq, aq);
+    atomicAdd(db + qq, ab);
+  }
+}
+
+// Raw-exp multi-head attention backward, one workgroup per (sequence, head).
+// qkv rows of the sequence: s*L + i (per-token projection layout, ld = 3D);
+// dctx [rows, D]; writes dqkv [rows, 3D] slices of this head.
+template <int LMAX>
+__global__ __launch_bounds__(256) void mhsa_backward_kernel(const float* __restrict__ qkv,
+                                                            const float* __restrict__ dctx, int L,
+                                                            int D, int H,
+                                                            float* __restrict__ dqkv) {
+  constexpr int DK = 20;
+  __shared__ float sq[LMAX][DK], sk[LMAX][DK], sv[LMAX][DK], so[LMAX][DK];
+  __shared__ float sa[LMAX][LMAX + 1], sda[LMAX][LMAX + 1];
+  __shared__ float srow[LMAX];
+  const int64_t s = blockIdx.x / H;
+  const int h = blockIdx.x - (int)(s * H);
+  const int tid = threadIdx.x;
+  const int ld = 3 * D;
+  const float rs = 1.0f / sqrtf((float)DK);
+  for (int e = tid; e < L * DK; e += 256) {
+    const int i = e / DK, t = e - i * DK;
+    const float* row = qkv + (s * L + i) * ld + h * DK + t;
+    sq[i][t] = row[0];
+    sk[i][t] = row[D];
+    sv[i][t] = row[2 * D];
+    so[i][t] = dctx[(s * L + i) * D + h * DK + t];
+  }
+  __syncthreads();
+  // E_ij = exp(q_i k_j / sqrt(dk)) (no max subtraction, as the forward); dA_ij = dO_i . V_j
+  for (int e = tid; e < L * L; e += 256) {
+    const int i = e / L, j = e - i * L;
+    float d = 0.f, g = 0.f;
+#pragma unroll
+    for (int t = 0; t < DK; ++t) {
+      d = fmaf(sq[i][t], sk[j][t], d);
+      g = fmaf(so[i][t], sv[j][t], g);
+    }
+    sa[i][j] = expf(d * rs);
+    sda[i][j] = g;
+  }
+  __syncthreads();
+  // A = E / (Z + 1e-8); rowdot_i = sum_j dA_ij A_ij
+  if (tid < L) {
+    const int i = tid;
+    float z = 0.f;
+    for (int j = 0; j < L; ++j) z += sa[i][j];
+    const float inv = 1.0f / (z + 1e-8f);
+    float rd = 0.f;
+    for (int j = 0; j < L; ++j) {
+      const float a = sa[i][j] * inv;
+      sa[i][j] = a;
+      rd = fmaf(sda[i][j], a, rd);
+    }
+    srow[i] = rd;
+  }
+  __syncthreads();
+  // dV_j = sum_i A_ij dO_i
+  for (int e = tid; e < L * DK; e += 256) {
+    const int j = e / DK, t = e - j * DK;
+    float acc = 0.f;
+    for (int i = 0; i < L; ++i) acc = fmaf(sa[i][j], so[i][t], acc);
+    dqkv[(s * L + j) * ld + 2 * D + h * DK + t] = acc;
+  }
+  __syncthreads();
+  // dS_ij = A_ij (dA_ij - rowdot_i), scaled by 1/sqrt(dk) for dQ / dK
+  for (int e = tid; e < L * L; e += 256) {
+    const int i = e / L, j = e - i * L;
+    sda[i][j] = sa[i][j] * (sda[i][j] - srow[i]) * rs;
+  }
+  __syncthreads();
+  for (int e = tid; e < L * DK; e += 256) {
+    const int i = e / DK, t = e - i * DK;
+    float gq = 0.f, gk = 0.f;
+    for (int j = 0; j < L; ++j) {
+      gq = fmaf(sda[i][j], sk[j][t], gq);
+      gk = fmaf(sda[j][i], sq[j][t], gk);
+    }
+    dqkv[(s * L + i) * ld + h * DK + t] = gq;
+    dqkv[(s * L + i) * ld + D + h * DK + t] = gk;
+  }
+}
+
+// dW[n][k] += sum_r dY[r][n] X[r][k] (+ db[n] += sum_r dY[r][n] from the
+// column tile 0 blocks). f32 MFMA 16x16x4; block = 64 (n) x 64 (k) tile over a
+// 256-row slice, 4 waves each a 16-row (n) strip x 64 cols; LDS tiles of
+// 32 rows; the slice's partial sums go to global with atomics.
+constexpr int TN_TILE = 64, TN_ROWS = 256, TN_BK = 32;
+__global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ dY, int64_t R,
+                                                      int N, const float* __restrict__ X, int K,
+                                                      float* __restrict__ dW,
+                                                      float* __restrict__ db) {
+  __shared__ float sy[TN_BK][TN_TILE + 1], sx[TN_BK][TN_TILE + 1];
+  const int n0 = blockIdx.x * TN_TILE, k0 = blockIdx.y * TN_TILE;
+  const int64_t r0 = (int64_t)blockIdx.z * TN_ROWS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lm = lane & 15, kq = lane >> 4;
+  floatx4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  float bsum = 0.f;   // db: thread tid < 64 sums column n0 + tid
+  for (int rb = 0; rb < TN_ROWS; rb += TN_BK) {
+    for (int e = tid; e < TN_BK * TN_TILE; e += 256) {
+      const int rr = e / TN_TILE, c = e - rr * TN_TILE;
+      const int64_t r = r0 + rb + rr;
+      const bool rin = r < R;
+      sy[rr][c] = (rin && n0 + c < N) ? dY[r * N + n0 + c] : 0.f;
+      sx[rr][c] = (rin && k0 + c < K) ? X[r * K + k0 + c] : 0.f;
+    }
+    __syncthreads();
+    if (db && blockIdx.y == 0 && tid < TN_TILE)
+      for (int rr = 0; rr < TN_BK; ++rr) bsum += sy[rr][tid];
+#pragma unroll
+    for (int kk = 0; kk < TN_BK; kk += 4) {
+      // A[i = n][k = r] = dY[r][n], B[k = r][j = col] = X[r][col]
+      const float a = sy[kk + kq][16 * w + lm];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float b = sx[kk + kq][16 * j + lm];
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // C/D: col = lane & 15, row = 4 (lane >> 4) + reg
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 16 * w + 4 * kq + r, k = k0 + 16 * j + lm;
+      if (n < N && k < K) atomicAdd(dW + (int64_t)n * K + k, acc[j][r]);
+    }
+  if (db && blockIdx.y == 0 && tid < TN_TILE && n0 + tid < N) atomicAdd(db + n0 + tid, bsum);
+}
+
+// dtable[ids[t]] += dx[t] for ids[t] != padding_idx (nn.Embedding(padding_idx=0)
+// leaves that row's gradient zero). One wave per token row, 4 columns per lane.
+__global__ __launch_bounds__(256) void embedding_backward_kernel(
+    const int64_t* __restrict__ ids, int64_t n_tok, const float* __restrict__ dx, int64_t V,
+    int D, int64_t padding_idx, float* __restrict__ dtable) {
+  const int lane = threadIdx.x & 63;
+  const int64_t t = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (t >= n_tok) return;
+  const int64_t id = ids[t];
+  if (id == padding_idx || (uint64_t)id >= (uint64_t)V) return;
+  for (int d = lane; d < D; d += 64) atomicAdd(dtable + id * D + d, dx[t * D + d]);
+}
+
+// torch.optim.Adam (default, amsgrad = False, weight_decay = 0), in its
+// single-tensor operation order: m = lerp(m, g, 1 - b1); v = b2 v + (1 - b2) g^2;
+// denom = sqrt(v) / sqrt(1 - b2^t) + eps; p -= (lr / (1 - b1^t)) m / denom.
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
+                                                   const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   int64_t n, float lr, float b1, float b2,
+                                                   float eps, float bc1, float bc2_sqrt) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const float gi = g[i];
+  const float mi = m[i] + (1.0f - b1) * (gi - m[i]);
+  const float vi = v[i] * b2 + (1.0f - b2) * gi * gi;
+  m[i] = mi;
+  v[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  p[i] -= (lr / bc1) * (mi / denom);
+}
+
+// dst[c][r] = W[r][c] for the stacked segments W = [src_0; src_1; ...]
+// (seg_rows rows each, `cols` columns): the [in, out] copy of nn.Linear
+// weights that turns dX = dY W into the X W^T form of the store GEMM.
+__global__ __launch_bounds__(256) void transpose_kernel(const float* s0, const float* s1,
+                                                        const float* s2, int seg_rows, int rows,
+                                                        int cols, float* __restrict__ dst) {
+  __shared__ float t[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;   // 32 x 8
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, c = c0 + tx;
+    if (r < rows && c < cols) {
+      const int seg = r / seg_rows;
+      const float* src = seg == 0 ? s0 : (seg == 1 ? s1 : s2);
+      t[k][tx] = src[(int64_t)(r - seg * seg_rows) * cols + c];
+    }
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, r = r0 + tx;
+    if (r < rows && c < cols) dst[(int64_t)c * rows + r] = t[tx][k];
+  }
+}
+
+inline unsigned grid256(int64_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+int32_t launch_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, hipStream_t s) {
+  if (n == 0) return NRMS_OK;
+  const float scale = p < 1.f ? 1.0f / (1.0f - p) : 0.f;
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid256(n)), dim3(256), 0, s, x, y, n, p, scale, seed);
+  return launch_status();
+}
+
+int32_t launch_score_backward(const float* news, int64_t B, int C, int64_t sb, int64_t sc,
+                              const float* user, int64_t su, int D, const float* dl, float* dnews,
+                              float* duser, hipStream_t s) {
+  if (B == 0) return NRMS_OK;
+  hipLaunchKernelGGL(score_backward_kernel, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, s, news, B,
+                     C, sb, sc, user, su, D, dl, dnews, duser);
+  return launch_status();
+}
+
+int32_t launch_additive_backward_rows(const float* x, const float* y, const float* score,
+                                      const float* q, const float* dout, int64_t n_seq, int L,
+                                      int D, int Q, float* dx, float* dz, float* dq, float* db,
+                                      hipStream_t s) {
+  if (n_seq == 0) return NRMS_OK;
+  if (L < 1 || L > 64) return NRMS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(additive_backward_rows_kernel, dim3((unsigned)n_seq), dim3(256), 0, s, x, y,
+                     score, q, dout, L, D, Q, dx, dz, dq, db);
+  return launch_status();
+}
+
+int32_t launch_mhsa_backward(const float* qkv, const float* dctx, int64_t n_seq, int L, int D,
+                             int H, float* dqkv, hipStream_t s) {
+  if (n_seq == 0) return NRMS_OK;
+  if (D != 20 * H || L < 1 || L > 64) return NRMS_ERR_UNSUPPORTED;
+  const int64_t blocks = n_seq * H;
+  if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  if (L <= 20)
+    hipLaunchKernelGGL(mhsa_backward_kernel<20>, dim3((unsigned)blocks), dim3(256), 0, s, qkv, dctx,
+                       L, D, H, dqkv);
+  else
+    hipLaunchKernelGGL(mhsa_backward_kernel<64>, dim3((unsigned)blocks), dim3(256), 0, s, qkv, dctx,
+                       L, D, H, dqkv);
+  return launch_status();
+}
+
+int32_t launch_gemm_tn(const float* dY, int64_t R, int N, const float* X, int K, float* dW,
+                       float* db, hipStream_t s) {
+  if (R == 0) return NRMS_OK;
+  const int64_t zs = (R + TN_ROWS - 1) / TN_ROWS;
+  if (zs > 65535) return NRMS_ERR_UNSUPPORTED;
+  dim3 grid((N + TN_TILE - 1) / TN_TILE, (K + TN_TILE - 1) / TN_TILE, (unsigned)zs);
+  hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, dW, db);
+  return launch_status();
+}
+
+int32_t launch_transpose(const float* const* src, int nseg, int seg_rows, int cols, float* dst,
+                         hipStream_t s) {
+  const int rows = nseg * seg_rows;
+  if (rows == 0 || cols == 0) return NRMS_OK;
+  dim3 grid((cols + 31) / 32, (rows + 31) / 32);
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, s, src[0], nseg > 1 ? src[1] : src[0],
+                     nseg > 2 ? src[2] : src[0], seg_rows, rows, cols, dst);
+  return launch_status();
+}
+
+int32_t launch_embedding_backward(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
+                                  int D, int64_t padding_idx, float* dtable, hipStream_t s) {
+  if (n_tok == 0) return NRMS_OK;
+  hipLaunchKernelGGL(embedding_backward_kernel, dim3((unsigned)((n_tok + 3) / 4)), dim3(256), 0, s,
+                     ids, n_tok, dx, V, D, padding_idx, dtable);
+  return launch_status();
+}
+
+int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
+                    float b2, float eps, int64_t step, hipStream_t s) {
+  if (n == 0) return NRMS_OK;
+  // bias corrections in double then rounded, as torch computes them on the host
+  const float bc1 = (float)(1.0 - pow((double)b1, (double)step));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, (double)step));
+  hipLaunchKernelGGL(adam_kernel, dim3(grid256(n)), dim3(256), 0, s, p, g, m, v, n, lr, b1, b2, eps,
+                     bc1, bc2_sqrt);
+  return launch_status();
+}
+
+}  // namespace nrms

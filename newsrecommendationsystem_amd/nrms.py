@@ -227,6 +227,7 @@ class NRMS(nn.Module):
         self.user_encoder = UserEncoder(config)
         self.click_predictor = DotProductClickPredictor()
         self._ws = _Workspace()
+        self._train_calls = 0
 
     def forward(self, candidate_news, clicked_news):
         """candidate_news: list (1+K) of {"title": LongTensor[B, L]};
@@ -241,7 +242,14 @@ class NRMS(nn.Module):
         """Tensor form of forward: cand_ids [B, C, L], clicked_ids [B, N, L]."""
         ne = self.news_encoder
         if self.training:
-            return _train.forward_autograd(self, ne._ids(cand_ids), ne._ids(clicked_ids))
+            cand, clk = ne._ids(cand_ids), ne._ids(clicked_ids)
+            if cand.is_cuda and getattr(self.config, "hip_train", True):
+                # HIP train-mode forward + backward kernels (train_hip.py); one
+                # dropout seed per call, as torch's RNG advances per call
+                from . import train_hip
+                self._train_calls += 1
+                return train_hip.forward_hip(self, cand, clk, seed=self._train_calls)
+            return _train.forward_autograd(self, cand, clk)
         cand = ne._ids(cand_ids)
         clk = ne._ids(clicked_ids)
         B, C, L = cand.shape

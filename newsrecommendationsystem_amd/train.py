@@ -2,12 +2,11 @@
 BASELINE config 5 (one process per GPU, local Adam steps, parameter
 all-reduce over RCCL every E steps).
 
-Status: the scoring path (eval mode) is hand-written HIP; the TRAINING
-forward/backward here is the reference's own op sequence on ATen autograd
-(GPU kernels from PyTorch-ROCm, no HIP kernels of this package) — the HIP
-backward kernels are the next step. It exists so that
-src/train.py can drive this module as a drop-in and so config 5's FedAvg
-exchange is real: `FedAvg.sync()` averages the 21,955,400 fp32 parameters
+On a GPU the training step runs the HIP training kernels (train_hip.py:
+train-mode forward with dropout, backward, Adam). The functions below are the
+reference's own op sequence on ATen autograd: the CPU path, and the GPU
+tests' reference for the HIP gradients (tests/test_gpu_train.py). Config 5's
+FedAvg exchange: `FedAvg.sync()` averages the 21,955,400 fp32 parameters
 (87.8 MB) with one all-reduce. The reference has no federated averaging at all
 (SURVEY §0 finding 2), so there is no oracle for the averaged trajectory; the
 tests check the exchange itself (every rank ends with the exact mean) and the
@@ -86,9 +85,11 @@ def loss_fn(logits):
 
 
 def train_step(model, optimizer, cand_ids, clicked_ids):
-    """One iteration of the loop body of src/train.py:202-236."""
+    """One iteration of the loop body of src/train.py:202-236. On a GPU the
+    forward/backward are the HIP training kernels (model.forward_ids in train
+    mode -> train_hip.NRMSTrain); on the CPU, ATen autograd."""
     model.train()
-    logits = forward_autograd(model, cand_ids, clicked_ids, training=True)
+    logits = model.forward_ids(cand_ids, clicked_ids)
     loss = loss_fn(logits)
     optimizer.zero_grad()
     loss.backward()
@@ -139,6 +140,11 @@ class FedAvg:
 
 
 def make_optimizer(model):
+    """Adam(lr = config.learning_rate) (src/train.py:127): the HIP update
+    (train_hip.HipAdam, same state keys) on a GPU, torch.optim.Adam on CPU."""
+    if next(model.parameters()).is_cuda:
+        from .train_hip import HipAdam
+        return HipAdam(model.parameters(), lr=model.config.learning_rate)
     return torch.optim.Adam(model.parameters(), lr=model.config.learning_rate)
 
 
@@ -175,16 +181,26 @@ def _main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=128)
     ap.add_argument("--every", type=int, default=5)
+    ap.add_argument("--aten", action="store_true", help="ATen autograd + torch Adam instead of HIP")
+    ap.add_argument("--warmup", type=int, default=2)
     a = ap.parse_args()
     rank, world, local, distributed = init_from_env()
     dev = torch.device("cuda", local) if torch.cuda.is_available() else torch.device("cpu")
     if dev.type == "cuda":
         torch.cuda.set_device(dev)
     torch.manual_seed(0)                        # identical initial weights on every rank
-    model = NRMS(NRMSConfig, torch.randn(NRMSConfig.num_words, 300)).to(dev)
-    opt = make_optimizer(model)
+
+    class Cfg(NRMSConfig):
+        hip_train = not a.aten
+    model = NRMS(Cfg, torch.randn(NRMSConfig.num_words, 300)).to(dev)
+    opt = (torch.optim.Adam(model.parameters(), lr=Cfg.learning_rate) if a.aten
+           else make_optimizer(model))
     fed = FedAvg(model, a.every) if distributed else None
-    batches = synthetic_train_batches(100 + rank, a.steps, a.batch, NRMSConfig.num_words, device=dev)
+    batches = synthetic_train_batches(100 + rank, a.steps + a.warmup, a.batch, NRMSConfig.num_words,
+                                      device=dev)
+    for cand, clk in batches[:a.warmup]:
+        train_step(model, opt, cand, clk)
+    batches = batches[a.warmup:]
     sync_t = 0.0
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -203,7 +219,8 @@ def _main():
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if rank == 0:
-        print(json.dumps({"mode": "train (ATen autograd) + FedAvg", "world": world, "steps": a.steps,
+        print(json.dumps({"mode": ("train (HIP kernels)" if dev.type == "cuda" and not a.aten
+                                   else "train (ATen autograd)") + " + FedAvg", "world": world, "steps": a.steps,
                           "batch_per_rank": a.batch, "fedavg_every": a.every,
                           "steps_per_s": a.steps / dt, "samples_per_s": world * a.batch * a.steps / dt,
                           "fedavg_sync_s_total": sync_t, "final_loss": float(loss),
