@@ -37,7 +37,7 @@ __device__ __forceinline__ void gemm_tile(
   constexpr int B_PASSES = (BN * BK / 4 + kThreads - 1) / kThreads;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lrow = tid >> 3, lc4 = tid & 7;
 
   // Staging sources: one A row and one W row per pass per thread.
@@ -255,7 +255,7 @@ __device__ __forceinline__ void gemm_x6_tile(
   constexpr int A_PASSES = XBM * XBK / 4 / kThreads;              // 4
   constexpr int B_PASSES = (BN * XBK / 4 + kThreads - 1) / kThreads;
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave & 1, wn = wave >> 1;
   const int lrow = tid >> 3, lc4 = tid & 7;
 

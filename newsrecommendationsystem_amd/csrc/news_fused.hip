@@ -198,19 +198,22 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
 
-template <bool X6>
+// MODE 0: f32 MFMA additive GEMM, fp32 context tile. MODE 1: split-bf16 x6,
+// context stored as bf16 planes.
+template <int MODE>
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const float* __restrict__ qkv, RowMap rmap, int64_t n_groups, const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add,
     float* __restrict__ out NRMS_TIMING_PARAM) {
   using Off = QkvOffsets;
+  constexpr bool X6 = MODE == 1;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* ctxL = lds;                                   // f32: [80][SC]
   __bf16* ctxB = reinterpret_cast<__bf16*>(lds);       // x6:  [80][XRB] = hi | mid | lo planes
   float* part = X6 ? lds + FROWS * XRB / 2 : ctxL + FROWS * SC;   // [4][80] per-wave row partials
   const float** rowptr = reinterpret_cast<const float**>(part + 4 * FROWS);   // [2][80]
 
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float* zero_row = WaP + WAP_MAX;
   const float* nan_row = zero_row + ROW;
 
@@ -574,13 +577,14 @@ int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16) return NRMS_ERR_UNSUPPORTED;
   const bool x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6;
-  auto kern = x6 ? &fused_news_kernel<true> : &fused_news_kernel<false>;
-  const size_t lds_bytes = x6 ? LDS_BYTES_X6 : LDS_BYTES;
+  const int mode = x6 ? 1 : 0;
+  auto kern = mode == 1 ? &fused_news_kernel<1> : &fused_news_kernel<0>;
+  const size_t lds_bytes = mode == 1 ? LDS_BYTES_X6 : LDS_BYTES;
   static bool attr_done[2] = {false, false};
-  if (!attr_done[x6]) {
+  if (!attr_done[mode]) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    attr_done[x6] = true;
+    attr_done[mode] = true;
   }
   if (x6) {
     const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
