@@ -203,6 +203,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="separate MHSA / additive / pool kernels")
     ap.add_argument("--no-extras", action="store_true", help="skip the gather / config-2 figures")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="process-group backend for the barrier / max-over-ranks timing (nccl = RCCL); "
+                         "gloo lets several ranks share one GPU for a rehearsal")
     ap.add_argument("--gemm", choices=["x6", "f32"], default="x6",
                     help="GEMM arithmetic: split-bf16 x6 (fp32-accurate, default) or exact f32 MFMA")
     args = ap.parse_args()
@@ -212,12 +215,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
-    device = torch.device("cuda", local)
+    device = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(device)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from newsrecommendationsystem_amd import _native as Nat
     from newsrecommendationsystem_amd.pipeline import ForwardPlan
@@ -253,6 +259,8 @@ def main():
         elapsed = time.perf_counter() - t0
     if dist:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        if args.dist_backend != "nccl":
+            t = t.cpu()
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
