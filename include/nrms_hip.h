@@ -104,7 +104,8 @@ int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_id
  * :74-75): for sequence s, token i reads qkv row r(s,i) = tok_ids ?
  * tok_ids[s*L+i] : s*L+i (tok_ids index qkv's n_rows_qkv rows). Sequences
  * s >= n_seq_a take their ids from tok_ids_b + (s-n_seq_a)*L (NULL: same
- * array). ctx[s*L+i, :] is the [D] context row. L <= 64. */
+ * array). ctx[s*L+i, :] is the [D] context row. L <= 4096 (beyond 64 the
+ * K|V rows are read through L2 instead of LDS). */
 int32_t nrms_self_attention(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
                             int64_t n_seq_a, const int64_t* tok_ids_b, int64_t n_seq,
                             int32_t L, const nrms_encoder_weights_t* w, float* ctx,
@@ -164,6 +165,16 @@ size_t nrms_user_encode_workspace_size(int64_t B, int32_t N, int32_t D);
 int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N,
                          const nrms_encoder_weights_t* w, float* out, void* workspace,
                          size_t workspace_bytes, hipStream_t stream);
+
+/* Fused UserEncoder tail (user_encoder.py:15-26 after the projection): raw-exp
+ * MHSA over qkv[B*N, 3D] (row b*N + i) + additive attention + pooling, one
+ * workgroup per user, the context kept in LDS; out[B, D]. N <= 64, reference
+ * geometry (D = 300, H = 15, Q = 200). Used by nrms_user_encode and
+ * nrms_forward when it applies. Workspace: a packed copy of W_add. */
+size_t nrms_user_attention_pool_workspace_size(int64_t B, int32_t N, int32_t D);
+int32_t nrms_user_attention_pool(const float* qkv, int64_t B, int32_t N,
+                                 const nrms_encoder_weights_t* w, float* out, void* workspace,
+                                 size_t workspace_bytes, hipStream_t stream);
 
 /* DotProductClickPredictor.forward (src/model/general/click_predictor/
  * dot_product.py:8-19): out[b, c] = <news[b*stride_b + c*stride_c, :], user[b*stride_u, :]>,

@@ -16,6 +16,7 @@ ABI_VERSION = 1
 
 NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
 NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32 = 0, 1
+NRMS_OK, NRMS_ERR_INVALID_ARG, NRMS_ERR_UNSUPPORTED, NRMS_ERR_WORKSPACE, NRMS_ERR_HIP = 0, 1, 2, 3, 4
 GEMM_ARITH_NAMES = {NRMS_GEMM_SPLIT_BF16X6: "split-bf16x6", NRMS_GEMM_F32: "f32"}
 
 _p = ctypes.c_void_p
@@ -52,6 +53,8 @@ SIGNATURES = {
     "nrms_news_encode": (_i32, [_p, _i64, _i32, _p, _i64, _EW, _i32, _p, _p, _sz, _p]),
     "nrms_news_encode_folded_workspace_size": (_sz, [_i64, _i32, _i32]),
     "nrms_news_encode_folded": (_i32, [_p, _i64, _i32, _p, _i64, _EW, _p, _p, _sz, _p]),
+    "nrms_user_attention_pool_workspace_size": (_sz, [_i64, _i32, _i32]),
+    "nrms_user_attention_pool": (_i32, [_p, _i64, _i32, _EW, _p, _p, _sz, _p]),
     "nrms_user_encode_workspace_size": (_sz, [_i64, _i32, _i32]),
     "nrms_user_encode": (_i32, [_p, _i64, _i32, _EW, _p, _p, _sz, _p]),
     "nrms_score": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p]),

@@ -121,6 +121,77 @@ __global__ __launch_bounds__(NT) void mhsa_rawexp_kernel(
   }
 }
 
+// Histories longer than 64 (K|V no longer fit LDS next to the exps in
+// registers): K|V rows read through L2, the raw exps computed twice (a sum
+// pass, then an accumulate pass; expf is deterministic, so the weights equal a
+// single-pass evaluation). Same arithmetic order per (query, head) as above.
+constexpr int kLongThreads = 256;
+
+__global__ __launch_bounds__(kLongThreads) void mhsa_rawexp_long_kernel(
+    const float* __restrict__ qkv, int64_t n_rows, const int64_t* __restrict__ ids_a,
+    int64_t n_seq_a, const int64_t* __restrict__ ids_b, int L, float* __restrict__ ctx) {
+  constexpr int DK = 20, H = 15, D = H * DK, ld = 3 * D;
+  extern __shared__ __attribute__((aligned(16))) int64_t lrow[];   // [L] row ids
+  const int64_t s = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t* ids = nullptr;
+  if (ids_a) ids = (s < n_seq_a || ids_b == nullptr) ? ids_a + s * L : ids_b + (s - n_seq_a) * L;
+  for (int i = tid; i < L; i += kLongThreads) {
+    const int64_t r = ids ? ids[i] : s * L + i;
+    lrow[i] = ((uint64_t)r < (uint64_t)n_rows) ? r : -1;
+  }
+  __syncthreads();
+  const float rs = 1.0f / sqrtf((float)DK);
+  for (int task = tid; task < L * H; task += kLongThreads) {
+    const int h = task / L;
+    const int i = task - h * L;
+    const int64_t r = lrow[i];
+    float q[DK];
+#pragma unroll
+    for (int t = 0; t < DK / 4; ++t) {
+      const float4 v = r >= 0 ? reinterpret_cast<const float4*>(qkv + r * ld + h * DK)[t] : nan4();
+      q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
+    }
+    auto raw = [&](int j) {
+      const int64_t rj = lrow[j];
+      float d = 0.f;
+#pragma unroll
+      for (int t = 0; t < DK / 4; ++t) {
+        const float4 k4 = rj >= 0 ? reinterpret_cast<const float4*>(qkv + rj * ld + D + h * DK)[t]
+                                  : nan4();
+        d = fmaf(q[4 * t], k4.x, d);
+        d = fmaf(q[4 * t + 1], k4.y, d);
+        d = fmaf(q[4 * t + 2], k4.z, d);
+        d = fmaf(q[4 * t + 3], k4.w, d);
+      }
+      return expf(d * rs);
+    };
+    float sum = 0.f;
+    for (int j = 0; j < L; ++j) sum += raw(j);
+    const float inv = 1.0f / (sum + 1e-8f);
+    float acc[DK];
+#pragma unroll
+    for (int t = 0; t < DK; ++t) acc[t] = 0.f;
+    for (int j = 0; j < L; ++j) {
+      const float a = raw(j) * inv;
+      const int64_t rj = lrow[j];
+#pragma unroll
+      for (int t = 0; t < DK / 4; ++t) {
+        const float4 v4 = rj >= 0
+            ? reinterpret_cast<const float4*>(qkv + rj * ld + 2 * D + h * DK)[t] : nan4();
+        acc[4 * t] = fmaf(a, v4.x, acc[4 * t]);
+        acc[4 * t + 1] = fmaf(a, v4.y, acc[4 * t + 1]);
+        acc[4 * t + 2] = fmaf(a, v4.z, acc[4 * t + 2]);
+        acc[4 * t + 3] = fmaf(a, v4.w, acc[4 * t + 3]);
+      }
+    }
+    float4* op = reinterpret_cast<float4*>(ctx + (s * L + i) * D + h * DK);
+#pragma unroll
+    for (int t = 0; t < DK / 4; ++t)
+      op[t] = make_float4(acc[4 * t], acc[4 * t + 1], acc[4 * t + 2], acc[4 * t + 3]);
+  }
+}
+
 constexpr int kPoolThreads = 256;
 
 __global__ __launch_bounds__(kPoolThreads) void additive_pool_kernel(
@@ -129,14 +200,36 @@ __global__ __launch_bounds__(kPoolThreads) void additive_pool_kernel(
   const int lane = threadIdx.x & 63;
   const int64_t s = (int64_t)blockIdx.x * (kPoolThreads / kWave) + (threadIdx.x >> 6);
   if (s >= n_seq) return;
-  const float v = lane < L ? score[s * L + lane] : -INFINITY;
+  const float* sc = score + s * L;
+  const int d4 = D / 4;
+  const float4* xs = reinterpret_cast<const float4*>(x + s * L * D);
+  float4* os = reinterpret_cast<float4*>(out + s * D);
+  if (L > kWave) {   // long sequence: strided max / sum, weights recomputed per row
+    float m = -INFINITY;
+    for (int l = lane; l < L; l += kWave) m = nan_max(m, sc[l]);
+    m = wave_max_nan(m);
+    float se = 0.f;
+    for (int l = lane; l < L; l += kWave) se += expf(sc[l] - m);
+    const float sum = wave_sum(se);
+    for (int c = lane; c < d4; c += kWave) {
+      float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int l = 0; l < L; ++l) {
+        const float wl = expf(sc[l] - m) / sum;
+        const float4 xv = xs[(int64_t)l * d4 + c];
+        acc.x = fmaf(wl, xv.x, acc.x);
+        acc.y = fmaf(wl, xv.y, acc.y);
+        acc.z = fmaf(wl, xv.z, acc.z);
+        acc.w = fmaf(wl, xv.w, acc.w);
+      }
+      os[c] = acc;
+    }
+    return;
+  }
+  const float v = lane < L ? sc[lane] : -INFINITY;
   const float m = wave_max_nan(v);
   const float e = lane < L ? expf(v - m) : 0.f;
   const float sum = wave_sum(e);
   const float w = e / sum;
-  const int d4 = D / 4;
-  const float4* xs = reinterpret_cast<const float4*>(x + s * L * D);
-  float4* os = reinterpret_cast<float4*>(out + s * D);
   // The shuffle must run with every lane active (a bpermute from an inactive
   // lane reads garbage), so the column guard sits inside the l-loop.
   for (int c0 = 0; c0 < d4; c0 += kWave) {
@@ -181,9 +274,14 @@ int32_t launch_mhsa(const float* qkv, int64_t n_rows, const int64_t* ids_a, int6
                     hipStream_t s) {
   if (n_seq == 0) return NRMS_OK;
   // Compiled for the reference configuration: d_k = 20, 15 heads (config.py:34,45).
-  if (DK != 20 || H != 15 || L < 1 || L > 64) return NRMS_ERR_UNSUPPORTED;
+  if (DK != 20 || H != 15 || L < 1 || L > kMaxSeqLen) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv % 16) != 0 || ((uintptr_t)ctx % 16) != 0) return NRMS_ERR_UNSUPPORTED;
   if (n_seq > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  if (L > 64) {
+    hipLaunchKernelGGL(mhsa_rawexp_long_kernel, dim3((unsigned)n_seq), dim3(kLongThreads),
+                       (size_t)L * sizeof(int64_t), s, qkv, n_rows, ids_a, n_seq_a, ids_b, L, ctx);
+    return launch_status();
+  }
   if (L <= 20) return launch_mhsa_inst<20, 320>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
   if (L <= 32) return launch_mhsa_inst<32, 512>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
   if (L <= 50) return launch_mhsa_inst<50, 768>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
@@ -193,7 +291,7 @@ int32_t launch_mhsa(const float* qkv, int64_t n_rows, const int64_t* ids_a, int6
 int32_t launch_additive_pool(const float* x, const float* score, int64_t n_seq, int L, int D,
                              float* out, hipStream_t s) {
   if (n_seq == 0) return NRMS_OK;
-  if (L < 1 || L > 64 || D % 4 != 0) return NRMS_ERR_UNSUPPORTED;
+  if (L < 1 || L > kMaxSeqLen || D % 4 != 0) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)x % 16) != 0 || ((uintptr_t)out % 16) != 0) return NRMS_ERR_UNSUPPORTED;
   const int per = kPoolThreads / kWave;
   const int64_t blocks = (n_seq + per - 1) / per;

@@ -271,7 +271,27 @@ int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
 size_t nrms_user_encode_workspace_size(int64_t B, int32_t N, int32_t D) {
   if (B < 0 || N <= 0 || D <= 0) return 0;
   const size_t rows = (size_t)B * N;
-  return align_up(rows * 3 * D * 4) + align_up(rows * D * 4) + align_up(rows * 4);
+  return align_up(rows * 3 * D * 4) + align_up(rows * D * 4) + align_up(rows * 4) +
+         align_up(fused_user_packed_b_floats() * 4);
+}
+
+size_t nrms_user_attention_pool_workspace_size(int64_t B, int32_t N, int32_t D) {
+  if (B < 0 || N <= 0 || D <= 0) return 0;
+  return align_up(fused_user_packed_b_floats() * 4);
+}
+
+int32_t nrms_user_attention_pool(const float* qkv, int64_t B, int32_t N,
+                                 const nrms_encoder_weights_t* w, float* out, void* workspace,
+                                 size_t workspace_bytes, hipStream_t stream) {
+  if (B < 0 || N <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (!fused_user_supported(N, w->d_model, w->n_heads, w->query_dim)) return NRMS_ERR_UNSUPPORTED;
+  if (B == 0) return NRMS_OK;
+  if (!qkv || !out) return NRMS_ERR_INVALID_ARG;
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* wap = cv.floats(fused_user_packed_b_floats());
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  return launch_fused_user(qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
 }
 
 int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N,
@@ -287,10 +307,13 @@ int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N,
   float* qkv = cv.floats((size_t)rows * 3 * D);
   float* ctx = cv.floats((size_t)rows * D);
   float* scores = cv.floats((size_t)rows);
+  float* wap = cv.floats(fused_user_packed_b_floats());
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   int32_t st = launch_gemm_store(clicked, rows, nullptr, rows, D, qkv_rows(w), 3 * D, qkv, 3 * D,
                                  stream);
   if (st) return st;
+  if (fused_user_supported(N, D, w->n_heads, w->query_dim) && ((uintptr_t)out % 16) == 0)
+    return launch_fused_user(qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
   return encode_from_qkv(qkv, rows, nullptr, B, nullptr, B, N, w, ctx, scores, out, stream);
 }
 

@@ -31,6 +31,10 @@ __device__ __forceinline__ float4 nan4() {
   return make_float4(n, n, n, n);
 }
 
+// Longest title / history the inference kernels take (K|V of a sequence of
+// more than 64 rows are read through L2 instead of LDS).
+constexpr int kMaxSeqLen = 4096;
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -110,6 +114,10 @@ int32_t launch_embedding_backward(const int64_t* ids, int64_t n_tok, const float
 int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                     float b2, float eps, int64_t step, hipStream_t s);
 
+size_t fused_user_packed_b_floats();
+bool fused_user_supported(int L, int D, int H, int Q);
+int32_t launch_fused_user(const float* qkv, int64_t B, int L, const float* w_add, const float* b_add,
+                          const float* q_add, float* wap, float* out, hipStream_t s);
 size_t fused_news_packed_b_floats();
 bool fused_news_supported(int L, int D, int H, int Q);
 int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a,

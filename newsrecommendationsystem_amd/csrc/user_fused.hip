@@ -1,0 +1,410 @@
+// Fused UserEncoder tail (src/model/NRMS/user_encoder.py:15-26): raw-exp
+// MHSA over the clicked-news Q|K|V rows (multihead_self.py:15-23,74-75), the
+// additive projection tanh(ctx W^T + b)·q (additive.py:35-38), the softmax over
+// the N clicked positions and the pooling (:39,51-52) in one launch, one
+// workgroup per user. Replaces the mhsa / additive-score / pool stage kernels
+// and their two HBM round trips of the [B*N, 300] context.
+//
+// LDS holds one [LMAX][600] fp32 tile (153.6 KB at LMAX = 64):
+//   0. the user's K|V rows (qkv columns 300..899) are staged in it;
+//   1. every (head, query) pair is one thread (15 N <= blockDim): q slice in
+//      registers, the N raw exps in registers (no max subtraction, as the
+//      reference), / (sum + 1e-8), context slice accumulated in registers;
+//      after a barrier the context rows are written over the K|V tile, with
+//      columns 300..319 zeroed (K padding):
+//      MODE 1 writes the context as its exact three-way bf16 split (three
+//      planes of 320 per row, k in MFMA fragment order), MODE 0 as fp32;
+//   2. additive GEMM [N x 320] x [320 x 208]: split-bf16 x6 on
+//      v_mfma_f32_16x16x32_bf16 (MODE 1; lane (lm, kq) reads k = 32ks + 4kq +
+//      0..3 and 32ks + 16 + 4kq + 0..3 of each plane in one ds_read_b128,
+//      conflict-free at row stride 600 floats), W_add pre-split into bf16
+//      planes packed in the same K order; or exact f32 MFMA 16x16x4 (MODE 0). Wave w owns N-tiles w, w + NW, ...
+//      for all M-tiles (rows >= N read row N-1 and are dropped). Epilogue:
+//      per-row partials of q_n tanh(y + b_n), one LDS row per N-tile;
+//   3. softmax over the N rows (max-subtracted, F.softmax) and the pooling
+//      (two lanes per float4 column, combined by a lane shuffle).
+#include "nrms_common.hpp"
+
+namespace nrms {
+namespace {
+
+constexpr int UD = 300, UH = 15, UDK = 20, UQ = 200;
+constexpr int UKS = 10;                    // bf16 k-steps of 32 (K 300 -> 320)
+constexpr int UKG = 19;                    // f32 k-groups of 16 (K 300 -> 304)
+constexpr int UNT = 13;                    // N tiles (208 >= 200)
+constexpr int UWAP3 = UKS * UNT * 3 * 64 * 4;   // floats: [ks][nt][plane][lane][8 bf16]
+constexpr int UWAP1 = UKG * UNT * 64 * 4;       // floats: [kg][nt][lane][4]
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void usplit3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)x;
+  const float r = x - (float)hi;
+  mid = (__bf16)r;
+  lo = (__bf16)(r - (float)mid);
+}
+
+// W_add -> B fragments. x6: element i of lane (n = lane & 15, kq = lane >> 4)
+// is k = 32 ks + 4 kq + (i & 3) + 16 (i >> 2), three bf16 planes. f32: the
+// 16x16x4 layout of the news kernel, k = 16 kg + 4 kq + t.
+__global__ __launch_bounds__(256) void pack_user_b_kernel(const float* __restrict__ Wa,
+                                                          float* __restrict__ WaP, int x6) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (x6) {
+    if (idx >= UKS * UNT * 64 * 8) return;
+    const int i = idx & 7, lane = (idx >> 3) & 63, nt = (idx >> 9) % UNT, ks = (idx >> 9) / UNT;
+    const int n = 16 * nt + (lane & 15);
+    const int k = 32 * ks + 4 * (lane >> 4) + (i & 3) + 16 * (i >> 2);
+    const float v = (n < UQ && k < UD) ? Wa[n * UD + k] : 0.f;
+    __bf16 hi, mid, lo;
+    usplit3(v, hi, mid, lo);
+    __bf16* o = reinterpret_cast<__bf16*>(WaP) + (((ks * UNT + nt) * 3) * 64 + lane) * 8 + i;
+    o[0] = hi;
+    o[64 * 8] = mid;
+    o[2 * 64 * 8] = lo;
+  } else {
+    if (idx >= UWAP1) return;
+    const int t = idx & 3, lane = (idx >> 2) & 63, nt = (idx >> 8) % UNT, c = (idx >> 8) / UNT;
+    const int n = 16 * nt + (lane & 15), k = 16 * c + 4 * (lane >> 4) + t;
+    WaP[idx] = (n < UQ && k < UD) ? Wa[n * UD + k] : 0.f;
+  }
+}
+
+__device__ __forceinline__ float urow16_sum(float v) {
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
+  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+
+constexpr int URS = 2 * UD;                // LDS row stride: K|V, then context (conflict-free)
+constexpr int UKP = 320;                   // bf16 context plane width (K padded)
+
+// Position of context column k in a bf16 plane: within each 32-column block,
+// lane kq's eight fragment elements (k = 4kq + 0..3 and 16 + 4kq + 0..3) are
+// contiguous, so one ds_read_b128 per plane fetches them.
+__device__ __forceinline__ int ukpos(int k) {
+  return (k & ~31) + 8 * ((k & 15) >> 2) + 4 * ((k & 31) >> 4) + (k & 3);
+}
+
+template <int MODE, int LMAX, int NT>
+__global__ __launch_bounds__(NT, 1) void fused_user_kernel(
+    const float* __restrict__ qkv, int L, const float* __restrict__ WaP,
+    const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out) {
+  static_assert(NT >= UH * LMAX, "one (head, query) task per thread");
+  constexpr int NW = NT / 64;
+  constexpr int NTPW = (UNT + NW - 1) / NW;            // N-tiles per wave
+  constexpr int MT = (LMAX + 15) / 16;                 // M-tiles
+  extern __shared__ __attribute__((aligned(16))) float ulds[];
+  float* tile = ulds;                                  // [LMAX][URS]
+  float* part = tile + LMAX * URS;                     // [UNT][64]
+  float* wts = part + UNT * 64;                        // [64]
+  const int64_t s = blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const float* rows = qkv + s * L * 3 * UD;
+
+  // ---------------- 0. stage K|V (all loads in flight at once), q slices ----------------
+  const bool has = tid < UH * L;
+  const int h = has ? tid / L : 0, qi = has ? tid - h * L : 0;
+  float q[UDK];
+  {
+    const float4* qp = reinterpret_cast<const float4*>(rows + (size_t)qi * 3 * UD + UDK * h);
+#pragma unroll
+    for (int t = 0; t < UDK / 4; ++t) {
+      const float4 v = qp[t];
+      q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
+    }
+    constexpr int KV4 = URS / 4;                               // float4 per K|V row
+    constexpr int PER = (LMAX * KV4 + NT - 1) / NT;
+    float4 buf[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + k * NT;
+      const int i = e / KV4, c = e - i * KV4;
+      buf[k] = e < L * KV4 ? *reinterpret_cast<const float4*>(rows + (size_t)i * 3 * UD + UD + 4 * c)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = tid + k * NT;
+      const int i = e / KV4, c = e - i * KV4;
+      if (e < L * KV4) *reinterpret_cast<float4*>(tile + i * URS + 4 * c) = buf[k];
+    }
+  }
+  __syncthreads();
+
+  // ---------------- 1. attention: thread = (head, query) ----------------
+  float acc[UDK];
+  if (has) {
+    const float rs = 1.0f / sqrtf((float)UDK);
+    // Keys j >= L read row L-1 and get weight 0 (no per-key branch, so the
+    // independent dot products interleave); adding 0 changes no sum.
+    auto raw = [&](int j) {
+      const int jj = j < L ? j : L - 1;
+      const float4* kr = reinterpret_cast<const float4*>(tile + jj * URS + UDK * h);
+      float d = 0.f;
+#pragma unroll
+      for (int t = 0; t < UDK / 4; ++t) {
+        const float4 k4 = kr[t];
+        d = fmaf(q[4 * t], k4.x, d);
+        d = fmaf(q[4 * t + 1], k4.y, d);
+        d = fmaf(q[4 * t + 2], k4.z, d);
+        d = fmaf(q[4 * t + 3], k4.w, d);
+      }
+      return j < L ? expf(d * rs) : 0.f;
+    };
+    // LMAX = 64 would not fit the exps in registers at 16 waves: recompute
+    // them in the second pass (expf is deterministic: same weights).
+    constexpr bool kKeep = LMAX <= 50;
+    float e[kKeep ? LMAX : 1];
+    constexpr int kUnroll = kKeep ? LMAX : 4;
+    float sum = 0.f;
+#pragma unroll kUnroll
+    for (int j = 0; j < LMAX; ++j) {
+      const float x = raw(j);
+      if constexpr (kKeep) e[j] = x;
+      sum += x;
+    }
+    const float inv = 1.0f / (sum + 1e-8f);
+#pragma unroll
+    for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
+#pragma unroll kUnroll
+    for (int j = 0; j < LMAX; ++j) {
+      const int jj = j < L ? j : L - 1;
+      float ej;
+      if constexpr (kKeep) ej = e[j]; else ej = raw(j);
+      const float a = ej * inv;
+      const float4* vr = reinterpret_cast<const float4*>(tile + jj * URS + UD + UDK * h);
+#pragma unroll
+      for (int t = 0; t < UDK / 4; ++t) {
+        const float4 v4 = vr[t];
+        acc[4 * t] = fmaf(a, v4.x, acc[4 * t]);
+        acc[4 * t + 1] = fmaf(a, v4.y, acc[4 * t + 1]);
+        acc[4 * t + 2] = fmaf(a, v4.z, acc[4 * t + 2]);
+        acc[4 * t + 3] = fmaf(a, v4.w, acc[4 * t + 3]);
+      }
+    }
+  }
+  __syncthreads();   // every K|V read done: the tile becomes the context
+  if constexpr (MODE == 1) {
+    // three bf16 planes per row (plane p at bf16 offset 320 p), k permuted to
+    // the MFMA fragment order: lane (lm, kq) of k-step ks reads 16 contiguous
+    // bytes per plane (see ukpos)
+    uint16_t* t16 = reinterpret_cast<uint16_t*>(tile);
+    if (has) {
+#pragma unroll
+      for (int g = 0; g < UDK / 4; ++g) {
+        uint16_t hv[3][4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          __bf16 h0, h1, h2;
+          usplit3(acc[4 * g + x], h0, h1, h2);
+          hv[0][x] = __builtin_bit_cast(uint16_t, h0);
+          hv[1][x] = __builtin_bit_cast(uint16_t, h1);
+          hv[2][x] = __builtin_bit_cast(uint16_t, h2);
+        }
+        const int pos = qi * (2 * URS) + ukpos(UDK * h + 4 * g);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          *reinterpret_cast<uint2*>(t16 + pos + UKP * pl) =
+              make_uint2(hv[pl][0] | ((uint32_t)hv[pl][1] << 16), hv[pl][2] | ((uint32_t)hv[pl][3] << 16));
+      }
+    }
+    for (int e = tid; e < L * 15; e += NT) {   // K padding 300..319, each plane
+      const int i = e / 15, g = (e % 15) % 5, pl = (e % 15) / 5;
+      *reinterpret_cast<uint2*>(t16 + i * (2 * URS) + UKP * pl + ukpos(UD + 4 * g)) = make_uint2(0u, 0u);
+    }
+  } else {
+    if (has) {
+      float4* dst = reinterpret_cast<float4*>(tile + qi * URS + UDK * h);
+#pragma unroll
+      for (int t = 0; t < UDK / 4; ++t)
+        dst[t] = make_float4(acc[4 * t], acc[4 * t + 1], acc[4 * t + 2], acc[4 * t + 3]);
+    }
+    for (int e = tid; e < L * 5; e += NT)   // K padding 300..319
+      *reinterpret_cast<float4*>(tile + (e / 5) * URS + UD + 4 * (e % 5)) = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+
+  // ---------------- 2. additive GEMM + tanh·q row partials ----------------
+  if (w < UNT) {
+    const int lm = lane & 15, kq = lane >> 4;
+    float qv[NTPW], bv[NTPW];
+#pragma unroll
+    for (int j = 0; j < NTPW; ++j) {
+      const int nt = w + NW * j;
+      const int col = 16 * nt + lm;
+      const bool ok = nt < UNT && col < UQ;
+      qv[j] = ok ? q_add[col] : 0.f;
+      bv[j] = ok ? b_add[col] : 0.f;
+    }
+    int arow[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int r = 16 * mt + lm;
+      arow[mt] = (r < L ? r : L - 1) * URS;
+    }
+    floatx4 c[MT][NTPW];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < NTPW; ++j) c[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+    if constexpr (MODE == 1) {
+      const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
+      const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile);
+      for (int ks = 0; ks < UKS; ++ks) {
+        bf16x8 a[MT][3];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            a[mt][pl] = *reinterpret_cast<const bf16x8*>(t16 + 2 * arow[mt] + UKP * pl + 32 * ks + 8 * kq);
+#pragma unroll
+        for (int j = 0; j < NTPW; ++j) {
+          const int nt = w + NW * j;
+          if (nt >= UNT) break;
+          bf16x8 b[3];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl) b[pl] = Bq[((ks * UNT + nt) * 3 + pl) * 64];
+#define NRMS_UX6(PA, PB)                                                                            \
+  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                                 \
+      c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], b[PB], c[mt][j], 0, 0, 0);
+          NRMS_UX6(2, 0) NRMS_UX6(1, 1) NRMS_UX6(0, 2) NRMS_UX6(1, 0) NRMS_UX6(0, 1) NRMS_UX6(0, 0)
+#undef NRMS_UX6
+        }
+      }
+    } else {
+      const float4* Bp = reinterpret_cast<const float4*>(WaP) + lane;
+      for (int cg = 0; cg < UKG; ++cg) {
+        float4 a[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          a[mt] = *reinterpret_cast<const float4*>(tile + arow[mt] + 16 * cg + 4 * kq);
+#pragma unroll
+        for (int j = 0; j < NTPW; ++j) {
+          const int nt = w + NW * j;
+          if (nt >= UNT) break;
+          const float4 b = Bp[(cg * UNT + nt) * 64];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt].x, b.x, c[mt][j], 0, 0, 0);
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt].y, b.y, c[mt][j], 0, 0, 0);
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt].z, b.z, c[mt][j], 0, 0, 0);
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt].w, b.w, c[mt][j], 0, 0, 0);
+          }
+        }
+      }
+    }
+    // C/D layout: col = lane & 15, row = 4 (lane >> 4) + reg; one partial row per N-tile
+#pragma unroll
+    for (int j = 0; j < NTPW; ++j) {
+      const int nt = w + NW * j;
+      if (nt >= UNT) break;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = urow16_sum(qv[j] * tanhf(c[mt][j][r] + bv[j]));
+          if (lm == 0) part[nt * 64 + 16 * mt + 4 * kq + r] = p;
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---------------- 3. softmax over the L rows + pooling ----------------
+  if (w == 0) {
+    float v = -INFINITY;
+    if (lane < L) {
+      v = part[lane];
+#pragma unroll
+      for (int nt = 1; nt < UNT; ++nt) v += part[nt * 64 + lane];
+    }
+    const float mx = wave_max_nan(v);
+    const float ex = lane < L ? expf(v - mx) : 0.f;
+    wts[lane] = ex / wave_sum(ex);
+  }
+  __syncthreads();
+  // two lanes per float4 column (rows of one parity each), 150 lanes in 3 waves
+  if (tid < 192) {
+    const int u = tid >> 1, par = tid & 1;
+    float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (u < UD / 4) {
+      for (int i = par; i < L; i += 2) {
+        const float wi = wts[i];
+        float4 cv;
+        if constexpr (MODE == 1) {   // hi + mid + lo == the fp32 context exactly
+          const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile) + i * (2 * URS) + ukpos(4 * u);
+          const uint2 p0 = *reinterpret_cast<const uint2*>(t16);
+          const uint2 p1 = *reinterpret_cast<const uint2*>(t16 + UKP);
+          const uint2 p2 = *reinterpret_cast<const uint2*>(t16 + 2 * UKP);
+          auto f = [](uint32_t wd, int hi) { return __uint_as_float(hi ? (wd & 0xffff0000u) : (wd << 16)); };
+          cv.x = (f(p0.x, 0) + f(p1.x, 0)) + f(p2.x, 0);
+          cv.y = (f(p0.x, 1) + f(p1.x, 1)) + f(p2.x, 1);
+          cv.z = (f(p0.y, 0) + f(p1.y, 0)) + f(p2.y, 0);
+          cv.w = (f(p0.y, 1) + f(p1.y, 1)) + f(p2.y, 1);
+        } else {
+          cv = *reinterpret_cast<const float4*>(tile + i * URS + 4 * u);
+        }
+        o.x = fmaf(wi, cv.x, o.x);
+        o.y = fmaf(wi, cv.y, o.y);
+        o.z = fmaf(wi, cv.z, o.z);
+        o.w = fmaf(wi, cv.w, o.w);
+      }
+    }
+    o.x += __shfl_xor(o.x, 1);
+    o.y += __shfl_xor(o.y, 1);
+    o.z += __shfl_xor(o.z, 1);
+    o.w += __shfl_xor(o.w, 1);
+    if (u < UD / 4 && par == 0) reinterpret_cast<float4*>(out + s * UD)[u] = o;
+  }
+}
+
+template <int MODE, int LMAX, int NT>
+int32_t launch_user_inst(const float* qkv, int64_t B, int L, const float* wap, const float* b_add,
+                         const float* q_add, float* out, hipStream_t s) {
+  const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64) * 4;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
+                     L, wap, b_add, q_add, out);
+  return launch_status();
+}
+
+template <int MODE>
+int32_t launch_user_mode(const float* qkv, int64_t B, int L, const float* wap, const float* b_add,
+                         const float* q_add, float* out, hipStream_t s) {
+  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, B, L, wap, b_add, q_add, out, s);
+  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, B, L, wap, b_add, q_add, out, s);
+  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, B, L, wap, b_add, q_add, out, s);
+  return launch_user_inst<MODE, 64, 1024>(qkv, B, L, wap, b_add, q_add, out, s);
+}
+
+}  // namespace
+
+size_t fused_user_packed_b_floats() { return (size_t)(UWAP3 > UWAP1 ? UWAP3 : UWAP1); }
+
+bool fused_user_supported(int L, int D, int H, int Q) {
+  return L >= 1 && L <= 64 && D == UD && H == UH && Q == UQ;
+}
+
+int32_t launch_fused_user(const float* qkv, int64_t B, int L, const float* w_add, const float* b_add,
+                          const float* q_add, float* wap, float* out, hipStream_t s) {
+  if (B == 0) return NRMS_OK;
+  if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16) return NRMS_ERR_UNSUPPORTED;
+  const int x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6 ? 1 : 0;
+  const int npk = x6 ? UKS * UNT * 64 * 8 : UWAP1;
+  hipLaunchKernelGGL(pack_user_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap, x6);
+  if (int32_t st = launch_status()) return st;
+  if (x6) return launch_user_mode<1>(qkv, B, L, wap, b_add, q_add, out, s);
+  return launch_user_mode<0>(qkv, B, L, wap, b_add, q_add, out, s);
+}
+
+}  // namespace nrms

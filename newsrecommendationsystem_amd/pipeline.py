@@ -12,7 +12,11 @@ Stage order (forward semantics, src/model/NRMS/__init__.py:19-48):
                 titles in one kernel (nrms_news_attention_pool); with
                 fused=False the three separate stages instead:
                 mhsa_news / addscore_news / pool_news
-  qkv_user / mhsa_user / addscore_user / pool_user   the UserEncoder
+  qkv_user      Q|K|V projection of the clicked news vectors
+  user_fused    raw-exp MHSA + additive attention + pooling per user in one
+                kernel (nrms_user_attention_pool); with fused=False (or a
+                shape the fused kernel does not take): mhsa_user /
+                addscore_user / pool_user
   score         dot-product click predictor
 """
 import ctypes
@@ -50,12 +54,17 @@ class ForwardPlan:
         self.wn, self._keep_n = ne.weights()
         self.wu, self._keep_u = model.user_encoder.weights()
         self.fused = fused
+        lib = N.load()
+        self.user_fused = fused and n_clicked <= 64 and D == D_MODEL
         news_st = ["news_fused"] if fused else ["mhsa_news", "addscore_news", "pool_news"]
-        self.stages = ["qkv_news"] + news_st + ["qkv_user", "mhsa_user", "addscore_user",
-                                                "pool_user", "score"]
+        user_st = ["user_fused"] if self.user_fused else ["mhsa_user", "addscore_user", "pool_user"]
+        self.stages = ["qkv_news"] + news_st + ["qkv_user"] + user_st + ["score"]
         if fused:
-            nb = N.load().nrms_news_attention_pool_workspace_size(n_all, L, D)
+            nb = lib.nrms_news_attention_pool_workspace_size(n_all, L, D)
             self.fws = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+        if self.user_fused:
+            nb = lib.nrms_user_attention_pool_workspace_size(B, n_clicked, D)
+            self.uws = torch.empty(nb, dtype=torch.uint8, device=self.dev)
 
     def run(self, cand_ids, clicked_ids, events=None):
         """cand_ids [B,C,L], clicked_ids [B,N,L] int64 on the device. If
@@ -94,16 +103,22 @@ class ForwardPlan:
         rec(k)
         N.call("nrms_qkv_project", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), st)
         rec(k + 1)
-        N.call("nrms_self_attention", P(self.uqkv), n_clk, None, B, None, B, Nc, wu,
-               P(self.uctx), st)
-        rec(k + 2)
-        N.call("nrms_additive_scores", P(self.uctx), n_clk, wu, P(self.uscores), st)
-        rec(k + 3)
-        N.call("nrms_additive_pool", P(self.uctx), P(self.uscores), B, Nc, D, P(self.user), st)
-        rec(k + 4)
+        if self.user_fused:
+            N.call("nrms_user_attention_pool", P(self.uqkv), B, Nc, wu, P(self.user), P(self.uws),
+                   self.uws.numel(), st)
+            k += 1
+        else:
+            N.call("nrms_self_attention", P(self.uqkv), n_clk, None, B, None, B, Nc, wu,
+                   P(self.uctx), st)
+            rec(k + 2)
+            N.call("nrms_additive_scores", P(self.uctx), n_clk, wu, P(self.uscores), st)
+            rec(k + 3)
+            N.call("nrms_additive_pool", P(self.uctx), P(self.uscores), B, Nc, D, P(self.user), st)
+            k += 3
+        rec(k + 1)
         N.call("nrms_score", P(self.news[n_clk:]), B, C, C * D, D, P(self.user), D, D,
                P(self.logits), st)
-        rec(k + 5)
+        rec(k + 2)
         return self.logits
 
     # Algorithmic work per launch of each stage (SURVEY §8d conventions:
@@ -131,5 +146,8 @@ class ForwardPlan:
             "mhsa_user": dict(flop=att_flop(B, Nc), bytes=4 * n_clk * 4 * D),
             "addscore_user": dict(flop=2 * n_clk * D * Q, bytes=4 * (n_clk * (D + 1) + Q * D)),
             "pool_user": dict(flop=2 * n_clk * D, bytes=4 * (n_clk * (D + 1) + B * D)),
+            # fused user tail: q|k|v rows in, user vectors out (context stays in LDS)
+            "user_fused": dict(flop=att_flop(B, Nc) + 2 * n_clk * D * Q + 2 * n_clk * D,
+                               bytes=4 * (n_clk * 3 * D + B * D + Q * D)),
             "score": dict(flop=2 * B * C * D, bytes=4 * (B * C * D + B * D + B * C)),
         }

@@ -37,6 +37,8 @@ def stage_of(name, grid_threads, wg):
         return "pool_news" if blocks > 256 else "pool_user"
     if "score_kernel" in name:
         return "score"
+    if "fused_user" in name:
+        return "user_fused"
     if "fused_news" in name:
         return "news_fused"
     if "gather_rows_kernel" in name:

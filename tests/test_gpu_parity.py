@@ -191,7 +191,7 @@ def test_train_mode_forward_matches_hip_eval(golden, golden_state, device):
     assert np.abs(_np(tr) - ev).max() / np.abs(ev).max() < 1e-5
 
 
-@pytest.mark.parametrize("L", [1, 5, 20, 32, 50, 64])
+@pytest.mark.parametrize("L", [1, 5, 20, 32, 50, 64, 65, 130])
 def test_news_encoder_title_lengths_vs_oracle(device, L):
     V = 512
     sd = W.nrms_state(7, V)
@@ -376,3 +376,64 @@ def test_split_bf16x6_accuracy_matches_f32(device):
     x6, f32 = errs[N.NRMS_GEMM_SPLIT_BF16X6], errs[N.NRMS_GEMM_F32]
     assert x6[0] < 1e-5 and x6[1] < 1e-5, errs
     assert x6[0] <= 2 * f32[0] + 1e-7 and x6[1] <= 2 * f32[1] + 1e-7, errs
+
+
+@pytest.mark.parametrize("B,n_clk", [(3, 1), (5, 17), (257, 50), (4, 64)])
+def test_fused_user_tail_vs_stages(device, B, n_clk, gemm_mode):
+    """Fused UserEncoder tail (nrms_user_attention_pool) == the separate stage
+    kernels within fp32 reordering, and == the fp64 oracle, for history
+    lengths 1..64 (the kernel's range)."""
+    from newsrecommendationsystem_amd import _native as N
+    V = 300
+    sd = W.nrms_state(23, V)
+    m = _module(sd, V, device)
+    rng = np.random.default_rng(100 + n_clk)
+    vec = (0.3 * rng.standard_normal((B, n_clk, 300))).astype(np.float32)
+    x = torch.from_numpy(vec).to(device).reshape(B * n_clk, 300).contiguous()
+    w, keep = m.user_encoder.weights()
+    st = N.stream_handle(device)
+    lib = N.load()
+    uqkv = torch.empty(B * n_clk, 900, device=device)
+    N.call("nrms_qkv_project", N.ptr(x), B * n_clk, None, B * n_clk, ctypes.byref(w), N.ptr(uqkv), st)
+    out = torch.empty(B, 300, device=device)
+    nb = lib.nrms_user_attention_pool_workspace_size(B, n_clk, 300)
+    ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    N.call("nrms_user_attention_pool", N.ptr(uqkv), B, n_clk, ctypes.byref(w), N.ptr(out), N.ptr(ws),
+           nb, st)
+    ctx = torch.empty(B * n_clk, 300, device=device)
+    sc = torch.empty(B * n_clk, device=device)
+    ref = torch.empty(B, 300, device=device)
+    N.call("nrms_self_attention", N.ptr(uqkv), B * n_clk, None, B, None, B, n_clk, ctypes.byref(w),
+           N.ptr(ctx), st)
+    N.call("nrms_additive_attention", N.ptr(ctx), B, n_clk, ctypes.byref(w), N.ptr(sc), N.ptr(ref),
+           st)
+    err = ((out - ref).norm(dim=1) / ref.norm(dim=1)).max()
+    assert err < 1e-5, float(err)
+    oracle = O.user_encode(vec, sd, np.float64)
+    assert O.normwise_rel_err(_np(out), oracle).max() < 1e-5
+    # the module path (nrms_user_encode) takes the fused kernel: bitwise equal
+    with torch.no_grad():
+        u = m.get_user_vector(torch.from_numpy(vec).to(device))
+    assert torch.equal(u, out)
+
+
+@pytest.mark.parametrize("n_clk", [65, 200])
+def test_user_tail_beyond_fused_range(device, n_clk):
+    """Histories longer than 64: the fused kernel declines (UNSUPPORTED) and
+    nrms_user_encode takes the stage kernels (K|V through L2, two-pass raw
+    exps, strided pooling softmax); result matches the oracle."""
+    from newsrecommendationsystem_amd import _native as N
+    V, B = 300, 3
+    sd = W.nrms_state(29, V)
+    m = _module(sd, V, device)
+    vec = (0.3 * np.random.default_rng(7).standard_normal((B, n_clk, 300))).astype(np.float32)
+    w, keep = m.user_encoder.weights()
+    lib = N.load()
+    out = torch.empty(B, 300, device=device)
+    x = torch.zeros(B * n_clk, 900, device=device)
+    rc = lib.nrms_user_attention_pool(N.ptr(x), B, n_clk, ctypes.byref(w), N.ptr(out), None, 0,
+                                      N.stream_handle(device))
+    assert rc == N.NRMS_ERR_UNSUPPORTED
+    with torch.no_grad():
+        u = _np(m.get_user_vector(torch.from_numpy(vec).to(device)))
+    assert O.normwise_rel_err(u, O.user_encode(vec, sd, np.float64)).max() < 1e-5
