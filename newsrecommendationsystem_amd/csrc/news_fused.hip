@@ -25,15 +25,20 @@
 //      conflict-free), B fragments from a pre-packed L2-resident copy of Wa
 //      (one global_load_dwordx4 per lane per 16-deep k-group and N tile);
 //      epilogue: per-row partials of sum_n q[n]·tanh(Y + b[n]) -> LDS.
-//   C  wave t <-> title t: softmax over the 20 tokens (max-subtracted, as
-//      F.softmax) and the pooling out[t] = sum_i w_i ctx[20t + i] from the
-//      same LDS tile.
+//   C  softmax over the 20 tokens (max-subtracted, as F.softmax) and pooling
+//      out[t] = sum_i w_i ctx[20t + i] from the attention's own O registers:
+//      the 4 lanes of a block hold all 20 rows of one (title, head), so both
+//      reduce inside the lane quad (DPP); the LDS tile is not read again.
 //
-// Three workgroup barriers per title group (after A, B and C).
+// Two workgroup barriers per title group (after A and after B); the next
+// group's q|k slices are loaded in the B epilogue, its V slices at the end
+// of C.
 // Output tile ownership in B (13 N-tiles x 5 M-tiles of 16x16): wave w owns
 // N-tiles 3w..3w+2 for all 5 M-tiles plus (M-tile w, N-tile 12); wave 0 also
 // (M-tile 4, N-tile 12).
 #include "nrms_common.hpp"
+
+#include <type_traits>
 
 namespace nrms {
 namespace {
@@ -194,6 +199,14 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// value of lane ^ 1 / lane ^ 2 within the quad (DPP quad_perm)
+__device__ __forceinline__ float quad_xor1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float quad_xor2(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
+}
+
 __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
   return __builtin_amdgcn_mfma_f32_4x4x1f32(a, b, c, 0, 0, 0);
 }
@@ -269,9 +282,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   const float* Aw = ctxL + lm * SC + 4 * kq;
 
   // q|k|v slices of one title group, lane (block (t, hl), x): Q / K of tokens
-  // x + 4j, V dims 5x..5x+4 of all 20 tokens. Loaded for the NEXT group at the
-  // start of the B epilogue, so the loads are in flight behind the tanh work,
-  // the pooling and two barriers instead of stalling the attention.
+  // x + 4j, V dims 5x..5x+4 of all 20 tokens. Loaded for the NEXT group: Q / K
+  // at the start of the B epilogue (in flight behind the tanh work, a barrier
+  // and the pooling), V at the end of C (behind the next S^T phase).
   float qf[5][FDK], kf[5][FDK], vf[FL][5];
   auto prefetch_qk = [&](int buf) {
 #pragma unroll
@@ -311,8 +324,13 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   int it = 0;
   for (int64_t tg = blockIdx.x; tg < n_groups; tg += gridDim.x, ++it) {
     const int nbuf = (it + 1) & 1;
-    __syncthreads();   // context tile free (pooling of the previous group done)
+    // (no barrier here: the context tile's last readers, the previous group's
+    // B mainloop, finished before its B -> C barrier; C reads registers + part)
+#ifdef NRMS_FUSED_TIMING
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // probe only: time the wait for this group's q|k|v
+#endif
     NRMS_STAMP(0)
+    floatx4 O[5][5];   // this wave's context rows, live until the pooling in C
 
     // ---------------- A: attention (4x4x1 MFMA, 16 (title, head) blocks) --------------
     {
@@ -352,7 +370,6 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           for (int r = 0; r < 4; ++r) S[j][i][r] *= inv;
       }
       // ctx^T tiles: rows = dims 5r' + m (A = V^T), cols = queries 4i + x (B = P^T)
-      floatx4 O[5][5];
 #pragma unroll
       for (int m = 0; m < 5; ++m)
 #pragma unroll
@@ -411,7 +428,6 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         // A fragments (16x16x32): lane holds A[row lm][32 ks + 8 kq .. + 7] of each plane
         const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
         const __bf16* Ab = ctxB + lm * XRB + 8 * kq;
-        bf16x8 bb[4][3], bn[4][3];
         auto load_b = [&](int ks, bf16x8 (&dst)[4][3]) {
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -420,9 +436,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
             for (int pl = 0; pl < 3; ++pl) dst[j][pl] = Bq[((ks * FNT + nt) * 3 + pl) * 64];
           }
         };
-        load_b(0, bb);
-        for (int ks = 0; ks < XKS; ++ks) {
-          if (ks + 1 < XKS) load_b(ks + 1, bn);
+        // one 32-deep k-step; EXTRA: wave 0 also owns (M-tile 4, N-tile 12)
+        auto kstep = [&](int ks, const bf16x8 (&bb)[4][3], auto extra) {
+          constexpr bool EXTRA = decltype(extra)::value;
           bf16x8 a[FMT][3], ax[3];
 #pragma unroll
           for (int mt = 0; mt < FMT; ++mt)
@@ -438,17 +454,25 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                          \
       acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);   \
   accX = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[PA], bb[3][PB], accX, 0, 0, 0);                      \
-  if (w == 0) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[FMT - 1][PA], bb[3][PB], accX2, 0, 0, 0);
+  if constexpr (EXTRA) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[FMT - 1][PA], bb[3][PB], accX2, 0, 0, 0);
           NRMS_X6STEP(2, 0) NRMS_X6STEP(1, 1) NRMS_X6STEP(0, 2) NRMS_X6STEP(1, 0) NRMS_X6STEP(0, 1)
           NRMS_X6STEP(0, 0)
 #undef NRMS_X6STEP
-          if (ks + 1 < XKS) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-#pragma unroll
-              for (int pl = 0; pl < 3; ++pl) bb[j][pl] = bn[j][pl];
+        };
+        // two B buffers in turn (XKS is even): no register copies between k-steps
+        auto mainloop = [&](auto extra) {
+          bf16x8 b0[4][3], b1[4][3];
+          load_b(0, b0);
+          for (int ks = 0; ks < XKS; ks += 2) {
+            load_b(ks + 1, b1);
+            kstep(ks, b0, extra);
+            if (ks + 2 < XKS) load_b(ks + 2, b0);
+            kstep(ks + 1, b1, extra);
           }
-        }
+        };
+        static_assert(XKS % 2 == 0, "k-steps in pairs");
+        if (w == 0) mainloop(std::true_type{});
+        else mainloop(std::false_type{});
       } else {
       float4 bb[4], bn[4];
 #pragma unroll
@@ -491,61 +515,71 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           if (xok && mt == w) p = fmaf(qx, tanh_fast(accX[r] + bx), p);
           if (xok && w == 0 && mt == FMT - 1) p = fmaf(qx, tanh_fast(accX2[r] + bx), p);
           p = row16_sum(p);
-          if (lm == 0) part[w * FROWS + 16 * mt + 4 * kq + r] = p;
+          if (lm == 0) part[4 * (16 * mt + 4 * kq + r) + w] = p;   // [row][wave]
         }
       }
-      prefetch_v(nbuf);
     }
     NRMS_STAMP(4)
     __syncthreads();   // row partials complete
     NRMS_STAMP(5)
 
-    // ---------------- C: softmax over tokens + pooling (wave t <-> title t) ----------------
+    // ---------------- C: softmax over tokens + pooling from the O registers ----------------
+    // Lane (block (at, hl), x) holds rows 4i + x (i < 5) of title at, head h:
+    // the 4 lanes of a block see all 20 tokens, so the softmax (max-subtracted,
+    // as F.softmax) and the pooling out[20h + d] = sum_l w_l ctx[l][20h + d]
+    // reduce within the lane quad (DPP); the LDS tile is not read.
     {
-      const int t = w;
-      const int64_t s = tg * FT + t;
-      const float v = lane < FL ? part[t * FL + lane] + part[FROWS + t * FL + lane] +
-                                      part[2 * FROWS + t * FL + lane] + part[3 * FROWS + t * FL + lane]
-                                : -INFINITY;
-      const float mx = wave_max_nan(v);
-      const float ex = lane < FL ? expf(v - mx) : 0.f;
-      const float wt = ex / wave_sum(ex);
-      float wts[FL];
+      float sc[5];
 #pragma unroll
-      for (int i = 0; i < FL; ++i) wts[i] = __shfl(wt, i);
-      if (s < rmap.n_titles) {
-#pragma unroll
-        for (int u0 = 0; u0 < 2; ++u0) {
-          const int u = lane + 64 * u0;   // float4 column of the 300-d output
-          if (u < FD / 4) {
-            const float* src = ctxL + FL * t * SC + 4 * u;
-            const __bf16* srcb = ctxB + FL * t * XRB + 4 * u;
-            float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int i = 0; i < FL; ++i) {
-              float4 cv;
-              if constexpr (X6) {
-                // hi + mid + lo reconstructs the fp32 context exactly
-                const bf16x4 vh = *reinterpret_cast<const bf16x4*>(srcb + i * XRB);
-                const bf16x4 vm = *reinterpret_cast<const bf16x4*>(srcb + i * XRB + XKP);
-                const bf16x4 vl = *reinterpret_cast<const bf16x4*>(srcb + i * XRB + 2 * XKP);
-                cv = make_float4(((float)vh[0] + (float)vm[0]) + (float)vl[0],
-                                 ((float)vh[1] + (float)vm[1]) + (float)vl[1],
-                                 ((float)vh[2] + (float)vm[2]) + (float)vl[2],
-                                 ((float)vh[3] + (float)vm[3]) + (float)vl[3]);
-              } else {
-                cv = *reinterpret_cast<const float4*>(src + i * SC);
-              }
-              acc.x = fmaf(wts[i], cv.x, acc.x);
-              acc.y = fmaf(wts[i], cv.y, acc.y);
-              acc.z = fmaf(wts[i], cv.z, acc.z);
-              acc.w = fmaf(wts[i], cv.w, acc.w);
-            }
-            reinterpret_cast<float4*>(out + s * FD)[u] = acc;
-          }
-        }
+      for (int i = 0; i < 5; ++i) {
+        const float4 pv = *reinterpret_cast<const float4*>(part + 4 * (FL * at + 4 * i + x));
+        sc[i] = ((pv.x + pv.y) + pv.z) + pv.w;
       }
-      // rowptr of the next title group (its previous readers finished before the B barrier)
+      float mx = sc[0];
+#pragma unroll
+      for (int i = 1; i < 5; ++i) mx = nan_max(mx, sc[i]);
+      mx = nan_max(mx, quad_xor1(mx));
+      mx = nan_max(mx, quad_xor2(mx));
+      float ex[5], sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        ex[i] = expf(sc[i] - mx);
+        sum += ex[i];
+      }
+      sum += quad_xor1(sum);
+      sum += quad_xor2(sum);
+      float wt[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) wt[i] = ex[i] / sum;
+      // pz[m][r'] = dim 5r' + m of head h, summed over this lane's 5 queries, then the quad
+      float pz[5][4];
+#pragma unroll
+      for (int m = 0; m < 5; ++m)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float a = 0.f;
+#pragma unroll
+          for (int i = 0; i < 5; ++i) a = fmaf(wt[i], O[m][i][r], a);
+          a += quad_xor1(a);
+          pz[m][r] = a + quad_xor2(a);
+        }
+      const int64_t s = tg * FT + at;
+      if (hval && s < rmap.n_titles) {
+        // lane x stores dims 5x .. 5x + 4 of head h
+        float v[5];
+#pragma unroll
+        for (int m = 0; m < 5; ++m)
+          v[m] = x == 0 ? pz[m][0] : (x == 1 ? pz[m][1] : (x == 2 ? pz[m][2] : pz[m][3]));
+        float* dst = out + s * FD + FDK * h + 5 * x;
+        float4_a4 v4;
+        v4.x = v[0]; v4.y = v[1]; v4.z = v[2]; v4.w = v[3];
+        *reinterpret_cast<float4_a4*>(dst) = v4;
+        dst[4] = v[4];
+      }
+      // V slices of the next group: issued here, after O is dead (holding both
+      // through the B epilogue spills); the S^T phase of the next group covers
+      // most of their latency (measured wait ~1.3k cycles per group)
+      prefetch_v(nbuf);
     }
     NRMS_STAMP(6)
   }

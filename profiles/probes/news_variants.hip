@@ -90,7 +90,7 @@ int main(int argc, char** argv) {
 #ifdef NRMS_FUSED_TIMING
     std::vector<unsigned long long> h_dbg(256 * 8 * 8);
     CK(hipMemcpy(h_dbg.data(), dbg, h_dbg.size() * 8, hipMemcpyDeviceToHost));
-    const char* names[7] = {"barrier0", "A", "barrier1", "B main", "B epi", "barrier2", "C"};
+    const char* names[7] = {"wait qk", "A", "barrier1", "B main", "B epi", "barrier2", "C"};
     const int nk = 7;
     for (int w = 0; w < nwaves[var]; ++w) {
       printf("  wave %d:", w);
