@@ -345,15 +345,18 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       for (int j = 0; j < 5; ++j)
 #pragma unroll
         for (int i = 0; i < 5; ++i) S[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      // One query column i at a time (S^T then exp; ctx^T then split + store):
+      // short live ranges, no spills. (Software-pipelining column i's VALU
+      // against column i + 1's MFMAs with sched_group_barrier measured slower:
+      // the longer live ranges spill in the B mainloop.)
+      auto s_mfma = [&](int i) {
 #pragma unroll
-      for (int d = 0; d < FDK; ++d)
+        for (int d = 0; d < FDK; ++d)
 #pragma unroll
-        for (int j = 0; j < 5; ++j)
-#pragma unroll
-          for (int i = 0; i < 5; ++i) S[j][i] = mfma4(kf[j][d], qf[i][d], S[j][i]);
+          for (int j = 0; j < 5; ++j) S[j][i] = mfma4(kf[j][d], qf[i][d], S[j][i]);
+      };
       // P = exp(S / sqrt(dk)) / (sum_keys + 1e-8): query 4i + x, key 4j + r
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
+      auto s_exp = [&](int i) {
         float sum = 0.f;
 #pragma unroll
         for (int j = 0; j < 5; ++j)
@@ -368,48 +371,57 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         for (int j = 0; j < 5; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) S[j][i][r] *= inv;
-      }
-      // ctx^T tiles: rows = dims 5r' + m (A = V^T), cols = queries 4i + x (B = P^T)
-#pragma unroll
-      for (int m = 0; m < 5; ++m)
-#pragma unroll
-        for (int i = 0; i < 5; ++i) O[m][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k = 0; k < FL; ++k)
-#pragma unroll
-        for (int m = 0; m < 5; ++m)
-#pragma unroll
-          for (int i = 0; i < 5; ++i) O[m][i] = mfma4(vf[k][m], S[k >> 2][i][k & 3], O[m][i]);
+      };
+      // ctx^T tiles: rows = dims 5r' + m (A = V^T), cols = queries 4i + x (B = P^T);
       // lane x holds ctx[query 4i + x][dim 5r' + m] = O[m][i][r']
-      if (hval) {
+      auto o_mfma = [&](int i) {
 #pragma unroll
-        for (int i = 0; i < 5; ++i) {
-          if constexpr (X6) {
-            __bf16* dst = ctxB + (FL * at + 4 * i + x) * XRB + FDK * h;
+        for (int m = 0; m < 5; ++m) O[m][i] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-            for (int c = 0; c < FDK / 4; ++c) {
-              bf16x4 vh, vm, vl;
+        for (int k = 0; k < FL; ++k)
 #pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const int d = 4 * c + e;
-                __bf16 a, b, cc;
-                split3(O[d % 5][i][d / 5], a, b, cc);
-                vh[e] = a; vm[e] = b; vl[e] = cc;
-              }
-              *reinterpret_cast<bf16x4*>(dst + 4 * c) = vh;
-              *reinterpret_cast<bf16x4*>(dst + XKP + 4 * c) = vm;
-              *reinterpret_cast<bf16x4*>(dst + 2 * XKP + 4 * c) = vl;
+          for (int m = 0; m < 5; ++m) O[m][i] = mfma4(vf[k][m], S[k >> 2][i][k & 3], O[m][i]);
+      };
+      // (a branch-free form, with the idle head slot storing its bit-identical
+      // copy of head 12, measured 9 % slower: the compiler then interleaves the
+      // stores into the next column's MFMAs and spills)
+      auto o_store = [&](int i) {
+        if (!hval) return;
+        if constexpr (X6) {
+          __bf16* dst = ctxB + (FL * at + 4 * i + x) * XRB + FDK * h;
+#pragma unroll
+          for (int c = 0; c < FDK / 4; ++c) {
+            bf16x4 vh, vm, vl;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int d = 4 * c + e;
+              __bf16 a, b, cc;
+              split3(O[d % 5][i][d / 5], a, b, cc);
+              vh[e] = a; vm[e] = b; vl[e] = cc;
             }
-          } else {
-            float4* dst = reinterpret_cast<float4*>(ctxL + (FL * at + 4 * i + x) * SC + FDK * h);
+            *reinterpret_cast<bf16x4*>(dst + 4 * c) = vh;
+            *reinterpret_cast<bf16x4*>(dst + XKP + 4 * c) = vm;
+            *reinterpret_cast<bf16x4*>(dst + 2 * XKP + 4 * c) = vl;
+          }
+        } else {
+          float4* dst = reinterpret_cast<float4*>(ctxL + (FL * at + 4 * i + x) * SC + FDK * h);
 #pragma unroll
-            for (int c = 0; c < FDK / 4; ++c) {
-              const int d0 = 4 * c;
-              dst[c] = make_float4(O[d0 % 5][i][d0 / 5], O[(d0 + 1) % 5][i][(d0 + 1) / 5],
-                                   O[(d0 + 2) % 5][i][(d0 + 2) / 5], O[(d0 + 3) % 5][i][(d0 + 3) / 5]);
-            }
+          for (int c = 0; c < FDK / 4; ++c) {
+            const int d0 = 4 * c;
+            dst[c] = make_float4(O[d0 % 5][i][d0 / 5], O[(d0 + 1) % 5][i][(d0 + 1) / 5],
+                                 O[(d0 + 2) % 5][i][(d0 + 2) / 5], O[(d0 + 3) % 5][i][(d0 + 3) / 5]);
           }
         }
+      };
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        s_mfma(i);
+        s_exp(i);
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        o_mfma(i);
+        o_store(i);
       }
       store_row(next_row, nbuf);
     }
