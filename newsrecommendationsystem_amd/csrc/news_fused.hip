@@ -286,28 +286,30 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   // at the start of the B epilogue (in flight behind the tanh work, a barrier
   // and the pooling), V at the end of C (behind the next S^T phase).
   float qf[5][FDK], kf[5][FDK], vf[FL][5];
-  auto prefetch_qk = [&](int buf) {
+  auto prefetch_qk_tok = [&](int buf, int j) {   // token x + 4j of the lane's title
+    const float* rp = rowptr[buf * FROWS + FL * at + x + 4 * j];
 #pragma unroll
-    for (int j = 0; j < 5; ++j) {
-      const float* rp = rowptr[buf * FROWS + FL * at + x + 4 * j];
-#pragma unroll
-      for (int c = 0; c < FDK / 4; ++c) {
-        const floatx4 a = *gptr<floatx4>(rp + Off::q(w, hls, c));
-        const floatx4 b = *gptr<floatx4>(rp + Off::k(w, hls, c));
-        qf[j][4 * c] = a.x; qf[j][4 * c + 1] = a.y; qf[j][4 * c + 2] = a.z; qf[j][4 * c + 3] = a.w;
-        kf[j][4 * c] = b.x; kf[j][4 * c + 1] = b.y; kf[j][4 * c + 2] = b.z; kf[j][4 * c + 3] = b.w;
-      }
+    for (int c = 0; c < FDK / 4; ++c) {
+      const floatx4 a = *gptr<floatx4>(rp + Off::q(w, hls, c));
+      const floatx4 b = *gptr<floatx4>(rp + Off::k(w, hls, c));
+      qf[j][4 * c] = a.x; qf[j][4 * c + 1] = a.y; qf[j][4 * c + 2] = a.z; qf[j][4 * c + 3] = a.w;
+      kf[j][4 * c] = b.x; kf[j][4 * c + 1] = b.y; kf[j][4 * c + 2] = b.z; kf[j][4 * c + 3] = b.w;
     }
   };
+  auto prefetch_qk = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) prefetch_qk_tok(buf, j);
+  };
   // (50 + 40 loads in two batches: at most 63 may be outstanding per wave)
+  auto prefetch_v_tok = [&](int buf, int k) {
+    const float* vr = rowptr[buf * FROWS + FL * at + k];
+    const float4_a4 a = *gptr<float4_a4>(vr + Off::v4(w, hls, x));
+    vf[k][0] = a.x; vf[k][1] = a.y; vf[k][2] = a.z; vf[k][3] = a.w;
+    vf[k][4] = *gptr<float>(vr + Off::v1(w, hls, x));
+  };
   auto prefetch_v = [&](int buf) {
 #pragma unroll
-    for (int k = 0; k < FL; ++k) {
-      const float* vr = rowptr[buf * FROWS + FL * at + k];
-      const float4_a4 a = *gptr<float4_a4>(vr + Off::v4(w, hls, x));
-      vf[k][0] = a.x; vf[k][1] = a.y; vf[k][2] = a.z; vf[k][3] = a.w;
-      vf[k][4] = *gptr<float>(vr + Off::v1(w, hls, x));
-    }
+    for (int k = 0; k < FL; ++k) prefetch_v_tok(buf, k);
   };
 
   if (blockIdx.x < n_groups) store_row(row_of(blockIdx.x), 0);
@@ -515,10 +517,15 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       }
       }
       NRMS_STAMP(3)
-      prefetch_qk(nbuf);
       // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
+      // The next group's Q|K slices go out one token per M-tile, between the
+      // tanh blocks (pinned by sched_barrier): issued all at once ahead of the
+      // tanh work, the in-order issue stalls the VALU behind the gather's
+      // address/TA queue (measured 3 % slower for the whole kernel).
 #pragma unroll
       for (int mt = 0; mt < FMT; ++mt) {
+        prefetch_qk_tok(nbuf, mt);
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float p = 0.f;
@@ -529,6 +536,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           p = row16_sum(p);
           if (lm == 0) part[4 * (16 * mt + 4 * kq + r) + w] = p;   // [row][wave]
         }
+        __builtin_amdgcn_sched_barrier(0);
       }
     }
     NRMS_STAMP(4)
