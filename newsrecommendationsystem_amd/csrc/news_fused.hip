@@ -67,12 +67,21 @@ constexpr size_t LDS_BYTES = LDS_FLOATS * sizeof(float);
 // the fp64 oracle) at 6/16 of the f32-MFMA time.
 constexpr int XKS = 10;                   // k-steps of 32 (K = 300 padded to 320)
 constexpr int XKP = XKS * 32;             // 320
-constexpr int XRB = 3 * XKP + 8;          // row stride in bf16 (1936 B = 16 x 121: conflict-free b128 rows)
+// Row stride in bf16: 976 (1,952 B = 488 dwords, = 8 mod 32 and 40 mod 64).
+// Conflict-free both ways: the A-fragment ds_read_b128 lane groups (16 rows x
+// 4 kq, bank = dword mod 64) cover all 64 banks once, and the attention's
+// ds_write_b64 plane stores (16-lane groups: 4 rows x 4 heads, bank = dword
+// mod 32) hit 16 distinct bank pairs. (968 = 484 dwords, = 4 mod 32, was
+// read-conflict-free but 2-way on the stores: 57 M conflict cycles/launch.)
+#ifndef NRMS_XRB_PAD
+#define NRMS_XRB_PAD 16
+#endif
+constexpr int XRB = 3 * XKP + NRMS_XRB_PAD;
 constexpr int WAP3_FLOATS = XKS * FNT * 3 * 64 * 4;   // [ks][nt][plane][lane][8 bf16]
 constexpr int WAP_MAX = WAP3_FLOATS > WAP_FLOATS ? WAP3_FLOATS : WAP_FLOATS;
 constexpr size_t LDS_BYTES_X6 = (size_t)FROWS * XRB * 2 + (4 * FROWS + 2 * 2 * FROWS) * sizeof(float);
 static_assert(LDS_BYTES_X6 <= 160 * 1024, "LDS (x6)");
-static_assert((FROWS * XRB * 2) % 16 == 0 && (XRB * 2) % 32 == 16, "x6 row stride");
+static_assert((FROWS * XRB * 2) % 16 == 0 && (XRB * 2) % 16 == 0, "x6 row stride");
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
