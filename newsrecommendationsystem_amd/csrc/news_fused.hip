@@ -356,10 +356,11 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       for (int j = 0; j < 5; ++j)
 #pragma unroll
         for (int i = 0; i < 5; ++i) S[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-      // One query column i at a time (S^T then exp; ctx^T then split + store):
-      // short live ranges, no spills. (Software-pipelining column i's VALU
-      // against column i + 1's MFMAs with sched_group_barrier measured slower:
-      // the longer live ranges spill in the B mainloop.)
+      // One query column i at a time (S^T, exp, ctx^T, split + store), so a
+      // column's S registers die before the next column's are written: short
+      // live ranges, no spills (all S^T first, then all ctx^T: 2 % slower;
+      // column i's split interleaved with column i + 1's MFMAs through
+      // sched_group_barrier: no better).
       auto s_mfma = [&](int i) {
 #pragma unroll
         for (int d = 0; d < FDK; ++d)
@@ -428,9 +429,6 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       for (int i = 0; i < 5; ++i) {
         s_mfma(i);
         s_exp(i);
-      }
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
         o_mfma(i);
         o_store(i);
       }
