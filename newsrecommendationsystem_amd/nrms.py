@@ -14,10 +14,12 @@ eager fallback: without the built library every call raises.
 Differences from the reference that a caller can observe:
   * the device is the module's own device (``.to(device)``), not a global
     ``cuda:0`` (src/model/NRMS/news_encoder.py:7), so one process per GPU works;
-  * training mode (``model.train()``) runs the reference's op sequence with
-    dropout on ATen autograd (newsrecommendationsystem_amd/train.py) so
-    src/train.py can drive this module; the HIP kernels are the eval-mode
-    scoring path (the north-star path) and the HIP backward is not built yet.
+  * training mode (``model.train()``) on a GPU runs the HIP training kernels
+    (train_hip.py: train-mode forward with dropout, backward through a
+    torch.autograd.Function) so src/train.py can drive this module unchanged;
+    on CPU (or with ``config.hip_train = False``) the reference's op sequence
+    runs on ATen autograd (newsrecommendationsystem_amd/train.py). Dropout
+    masks come from the library's counter-based generator, not torch's RNG.
 """
 import torch
 import torch.nn as nn
