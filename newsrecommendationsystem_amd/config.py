@@ -1,6 +1,6 @@
 """NRMS hyper-parameters, field-for-field with the reference's config classes
 (src/config.py:10-45) so a reference config object can be passed unchanged.
-Only the fields the NRMS path reads are listed, plus this build's own knobs
+The NRMS path and the preprocessing (preprocess.py) read these fields, plus this build's own knobs
 (prefixed ``hip_``)."""
 
 
@@ -14,10 +14,18 @@ class BaseConfig:
     num_clicked_news_a_user = 50
     num_words_title = 20
     num_words_abstract = 50
+    word_freq_threshold = 1
+    entity_freq_threshold = 2
+    entity_confidence_threshold = 0.5
     negative_sampling_ratio = 2
     dropout_probability = 0.2
     num_words = 1 + 70975
+    num_categories = 1 + 274
+    num_entities = 1 + 12957
+    num_users = 1 + 50000
     word_embedding_dim = 300
+    category_embedding_dim = 100
+    entity_embedding_dim = 100
     query_vector_dim = 200
 
 
