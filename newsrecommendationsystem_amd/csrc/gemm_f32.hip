@@ -234,16 +234,12 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void split4(const float4 v, bf16x4& h, bf16x4& m, bf16x4& l) {
-  const float x[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const __bf16 a = (__bf16)x[e];
-    const float r = x[e] - (float)a;
-    const __bf16 b = (__bf16)r;
-    h[e] = a;
-    m[e] = b;
-    l[e] = (__bf16)(r - (float)b);
-  }
+  uint32_t h0, m0, l0, h1, m1, l1;
+  split3x2(v.x, v.y, h0, m0, l0);
+  split3x2(v.z, v.w, h1, m1, l1);
+  h = __builtin_bit_cast(bf16x4, make_uint2(h0, h1));
+  m = __builtin_bit_cast(bf16x4, make_uint2(m0, m1));
+  l = __builtin_bit_cast(bf16x4, make_uint2(l0, l1));
 }
 
 template <int TNW>

@@ -403,17 +403,15 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           __bf16* dst = ctxB + (FL * at + 4 * i + x) * XRB + FDK * h;
 #pragma unroll
           for (int c = 0; c < FDK / 4; ++c) {
-            bf16x4 vh, vm, vl;
+            uint32_t h[2], m[2], l[2];
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int d = 4 * c + e;
-              __bf16 a, b, cc;
-              split3(O[d % 5][i][d / 5], a, b, cc);
-              vh[e] = a; vm[e] = b; vl[e] = cc;
+            for (int e = 0; e < 2; ++e) {
+              const int d = 4 * c + 2 * e;
+              split3x2(O[d % 5][i][d / 5], O[(d + 1) % 5][i][(d + 1) / 5], h[e], m[e], l[e]);
             }
-            *reinterpret_cast<bf16x4*>(dst + 4 * c) = vh;
-            *reinterpret_cast<bf16x4*>(dst + XKP + 4 * c) = vm;
-            *reinterpret_cast<bf16x4*>(dst + 2 * XKP + 4 * c) = vl;
+            *reinterpret_cast<uint2*>(dst + 4 * c) = make_uint2(h[0], h[1]);
+            *reinterpret_cast<uint2*>(dst + XKP + 4 * c) = make_uint2(m[0], m[1]);
+            *reinterpret_cast<uint2*>(dst + 2 * XKP + 4 * c) = make_uint2(l[0], l[1]);
           }
         } else {
           float4* dst = reinterpret_cast<float4*>(ctxL + (FL * at + 4 * i + x) * SC + FDK * h);

@@ -52,6 +52,24 @@ __device__ __forceinline__ float wave_max_nan(float v) {
   return v;
 }
 
+// Exact three-way bf16 split of two floats at once: x = hi + mid + lo with
+// each part the round-to-nearest bf16 of what the previous parts leave. The
+// paired conversion (one v_cvt_pk_bf16_f32 per plane per pair) and v_pk_add_f32
+// residuals take 4.5 VALU per element where converting one float at a time
+// takes about 8; the packed words come out as [x0 | x1 << 16] per plane.
+typedef __bf16 nrms_bf16x2 __attribute__((ext_vector_type(2)));
+typedef float nrms_f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split3x2(float x0, float x1, uint32_t& hi, uint32_t& mid,
+                                         uint32_t& lo) {
+  hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((nrms_f32x2){x0, x1}, nrms_bf16x2));
+  const float r0 = x0 - __builtin_bit_cast(float, hi << 16);
+  const float r1 = x1 - __builtin_bit_cast(float, hi & 0xffff0000u);
+  mid = __builtin_bit_cast(uint32_t, __builtin_convertvector((nrms_f32x2){r0, r1}, nrms_bf16x2));
+  const float s0 = r0 - __builtin_bit_cast(float, mid << 16);
+  const float s1 = r1 - __builtin_bit_cast(float, mid & 0xffff0000u);
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((nrms_f32x2){s0, s1}, nrms_bf16x2));
+}
+
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5, "XCD swizzle
 // must be bijective"): blocks dealt round-robin over 8 XCDs get contiguous
 // logical ids per XCD, so tiles that share operands share an L2.

@@ -195,20 +195,14 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     if (has) {
 #pragma unroll
       for (int g = 0; g < UDK / 4; ++g) {
-        uint16_t hv[3][4];
+        uint32_t hv[3][2];
 #pragma unroll
-        for (int x = 0; x < 4; ++x) {
-          __bf16 h0, h1, h2;
-          usplit3(acc[4 * g + x], h0, h1, h2);
-          hv[0][x] = __builtin_bit_cast(uint16_t, h0);
-          hv[1][x] = __builtin_bit_cast(uint16_t, h1);
-          hv[2][x] = __builtin_bit_cast(uint16_t, h2);
-        }
+        for (int x = 0; x < 2; ++x)
+          split3x2(acc[4 * g + 2 * x], acc[4 * g + 2 * x + 1], hv[0][x], hv[1][x], hv[2][x]);
         const int pos = qi * (2 * URS) + ukpos(UDK * h + 4 * g);
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
-          *reinterpret_cast<uint2*>(t16 + pos + UKP * pl) =
-              make_uint2(hv[pl][0] | ((uint32_t)hv[pl][1] << 16), hv[pl][2] | ((uint32_t)hv[pl][3] << 16));
+          *reinterpret_cast<uint2*>(t16 + pos + UKP * pl) = make_uint2(hv[pl][0], hv[pl][1]);
       }
     }
     for (int e = tid; e < L * 15; e += NT) {   // K padding 300..319, each plane
