@@ -218,10 +218,13 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_xwt_f32_kernel(
 // products, fp32 accumulation). Dropped terms are < 2^-25 |a||b| per product:
 // fp32-GEMM accuracy (tests compare against the fp64 oracle) at 6/16 of the
 // f32-MFMA cycles.
-// Block tile 128 x 192, K staged 32 deep (one bf16 k-step) with register
+// Block tile 64 x 192, K staged 32 deep (one bf16 k-step) with register
 // prefetch of the next chunk; 4 waves as 2 (rows) x 2 (cols), wave tile
-// 64 x (16 TNW); two workgroups per CU so one stages while the other computes.
-constexpr int XBM = 128;
+// 32 x (16 TNW); 148 VGPRs and 49 KB of LDS, so three workgroups share a CU
+// and stage while the others compute (the 128-row tile at 236 VGPRs, two per
+// CU, ran 3.5 % slower; 64 x 96 at four per CU no faster: its A tile is split
+// ten times per row instead of five).
+constexpr int XBM = 64;
 constexpr int XBK = 32;
 constexpr int XLD = 32;   // bf16 per LDS row (64 B, unpadded)
 // The 16-B chunk kq of row r sits at chunk kq ^ xsw(r): with 64-B rows this
@@ -242,13 +245,14 @@ __device__ __forceinline__ void split4(const float4 v, bf16x4& h, bf16x4& m, bf1
   l = __builtin_bit_cast(bf16x4, make_uint2(l0, l1));
 }
 
-template <int TNW>
+template <int TNW, int BMT>
 __device__ __forceinline__ void gemm_x6_tile(
     const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
     int64_t M, int K, const WeightRows& wr, int N, float* __restrict__ Y, int64_t ldy,
     int64_t m0, int n0, __bf16* __restrict__ As, __bf16* __restrict__ Bs) {
   constexpr int BN = 32 * TNW;
-  constexpr int A_PASSES = XBM * XBK / 4 / kThreads;              // 4
+  constexpr int A_PASSES = BMT * XBK / 4 / kThreads;              // 4 (BMT 128), 2 (64)
+  constexpr int MT = BMT / 32;                                   // 16-row tiles per wave
   constexpr int B_PASSES = (BN * XBK / 4 + kThreads - 1) / kThreads;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -300,8 +304,8 @@ __device__ __forceinline__ void gemm_x6_tile(
       const int r = lrow + 32 * p;
       __bf16* d = As + r * XLD + (((lc4 >> 1) ^ xsw(r)) << 3) + (lc4 & 1) * 4;
       *reinterpret_cast<bf16x4*>(d) = h;
-      *reinterpret_cast<bf16x4*>(d + XBM * XLD) = m;
-      *reinterpret_cast<bf16x4*>(d + 2 * XBM * XLD) = l;
+      *reinterpret_cast<bf16x4*>(d + BMT * XLD) = m;
+      *reinterpret_cast<bf16x4*>(d + 2 * BMT * XLD) = l;
     }
 #pragma unroll
     for (int p = 0; p < B_PASSES; ++p)
@@ -316,9 +320,9 @@ __device__ __forceinline__ void gemm_x6_tile(
       }
   };
 
-  floatx4 acc[4][TNW];
+  floatx4 acc[MT][TNW];
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt)
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int nt = 0; nt < TNW; ++nt) acc[mt][nt] = floatx4{0.f, 0.f, 0.f, 0.f};
   // N tiles of this wave past N hold no output: skip their MFMAs (wave-uniform)
@@ -331,7 +335,7 @@ __device__ __forceinline__ void gemm_x6_tile(
 
   const int lm = lane & 15, kq = lane >> 4;
   // rows 64 wm + 16 mt + lm and 16 TNW wn + 16 nt + lm all have xsw == xsw(lm)
-  const __bf16* Aw = As + (64 * wm + lm) * XLD + ((kq ^ xsw(lm)) << 3);
+  const __bf16* Aw = As + ((BMT / 2) * wm + lm) * XLD + ((kq ^ xsw(lm)) << 3);
   const __bf16* Bw = Bs + (16 * TNW * wn + lm) * XLD + ((kq ^ xsw(lm)) << 3);
 
   const int nk = (K + XBK - 1) / XBK;
@@ -340,12 +344,12 @@ __device__ __forceinline__ void gemm_x6_tile(
   __syncthreads();
   for (int kc = 0; kc < nk; ++kc) {
     if (kc + 1 < nk) gload(kc + 1);
-    bf16x8 a[4][3];
+    bf16x8 a[MT][3];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        a[mt][pl] = *reinterpret_cast<const bf16x8*>(Aw + pl * XBM * XLD + 16 * mt * XLD);
+        a[mt][pl] = *reinterpret_cast<const bf16x8*>(Aw + pl * BMT * XLD + 16 * mt * XLD);
 #pragma unroll
     for (int nt = 0; nt < TNW; ++nt) {
       if (nt >= nt_live) break;
@@ -355,7 +359,7 @@ __device__ __forceinline__ void gemm_x6_tile(
         b[pl] = *reinterpret_cast<const bf16x8*>(Bw + pl * BN * XLD + 16 * nt * XLD);
       // the six products with i + j <= 2, smallest first
 #define NRMS_X6(PA, PB)                                                                             \
-  _Pragma("unroll") for (int mt = 0; mt < 4; ++mt)                                                  \
+  _Pragma("unroll") for (int mt = 0; mt < MT; ++mt)                                                  \
       acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], b[PB], acc[mt][nt], 0, 0, 0);
       NRMS_X6(2, 0) NRMS_X6(1, 1) NRMS_X6(0, 2) NRMS_X6(1, 0) NRMS_X6(0, 1) NRMS_X6(0, 0)
 #undef NRMS_X6
@@ -368,7 +372,7 @@ __device__ __forceinline__ void gemm_x6_tile(
   }
 
   // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
-  const int64_t row_base = m0 + 64 * wm + kq * 4;
+  const int64_t row_base = m0 + (BMT / 2) * wm + kq * 4;
 #pragma unroll
   for (int nt = 0; nt < TNW; ++nt) {
     const int col = n0 + 16 * TNW * wn + 16 * nt + lm;
@@ -376,7 +380,7 @@ __device__ __forceinline__ void gemm_x6_tile(
     const int seg = col / wr.seg_rows;
     const float bias = wr.b[seg][col - seg * wr.seg_rows];
 #pragma unroll
-    for (int mt = 0; mt < 4; ++mt)
+    for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t row = row_base + 16 * mt + r;
@@ -388,7 +392,7 @@ __device__ __forceinline__ void gemm_x6_tile(
 // 192-wide column tiles; a last partial tile of <= 160 columns (N = 900:
 // 4 x 192 + 132) runs the 160-wide instantiation so its two wave columns
 // stay balanced (5 + 4 live N tiles instead of 6 + 3).
-__global__ __launch_bounds__(kThreads, 2) void gemm_x6_kernel(
+__global__ __launch_bounds__(kThreads, 3) void gemm_x6_kernel(
     const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
     int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy, int n_col_tiles) {
   __shared__ __attribute__((aligned(16))) __bf16 As[3 * XBM * XLD];
@@ -398,9 +402,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_x6_kernel(
   const int64_t m0 = (int64_t)(wg / n_col_tiles) * XBM;
   const int n0 = ct * 192;
   if (N - n0 > 160)
-    gemm_x6_tile<6>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
+    gemm_x6_tile<6, XBM>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
   else
-    gemm_x6_tile<5>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
+    gemm_x6_tile<5, XBM>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
 }
 
 constexpr int TN_STORE = 12;     // BN = 192: N = 900 -> 4 column tiles of 192 + one of 144

@@ -26,7 +26,7 @@ def stage_of(name, grid_threads, wg):
     """Map (kernel, grid) of the bench workload (B=1024, V=70976) to a stage."""
     blocks = grid_threads // max(wg, 1)
     if "gemm_xwt_f32_kernel<12, false>" in name or "gemm_x6" in name:
-        return "qkv_news" if blocks != 2000 else "qkv_user"
+        return "qkv_user" if blocks in (2000, 4000) else "qkv_news"   # M = 51,200: 128- or 64-row tiles
     if "gemm_xwt_f32_kernel<13" in name:
         return "addscore_news" if blocks > 400 else "addscore_user"
     if "mhsa_rawexp_kernel<20" in name:
