@@ -378,13 +378,16 @@ __device__ __forceinline__ void gemm_x6_tile(
     const int col = n0 + 16 * TNW * wn + 16 * nt + lm;
     if (col >= N) continue;
     const int seg = col / wr.seg_rows;
-    const float bias = wr.b[seg][col - seg * wr.seg_rows];
+    const float bias = wr.b[seg] ? wr.b[seg][col - seg * wr.seg_rows] : 0.f;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int64_t row = row_base + 16 * mt + r;
-        if (row < M) Y[row * ldy + col] = acc[mt][nt][r] + bias;
+        if (row < M) {
+          float* yp = Y + row * ldy + col;
+          *yp = (wr.accumulate ? *yp : 0.f) + acc[mt][nt][r] + bias;
+        }
       }
   }
 }
@@ -452,6 +455,9 @@ int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_i
 int32_t launch_gemm_store_f32(const float* X, int64_t M, int K, const WeightRows& w, int N, float* Y,
                               int64_t ldy, hipStream_t s) {
   if (M == 0) return NRMS_OK;
+  // the training dX GEMMs: split-bf16 x6 like the forward projections unless
+  // exact f32 MFMA is selected (NRMS_GEMM=f32)
+  if (gemm_arith() == NRMS_GEMM_SPLIT_BF16X6) return launch_gemm_store(X, M, nullptr, M, K, w, N, Y, ldy, s);
   if (K % 4 != 0 || ((uintptr_t)X % 16) != 0) return NRMS_ERR_UNSUPPORTED;
   for (int i = 0; i < w.nseg; ++i)
     if (((uintptr_t)w.w[i] % 16) != 0) return NRMS_ERR_UNSUPPORTED;

@@ -85,7 +85,7 @@ struct WeightRows {
   const float* b[3];   // may be null: no bias
   int seg_rows;
   int nseg;
-  int accumulate = 0;  // f32 store GEMM only: Y += X W^T (+ b)
+  int accumulate = 0;  // store GEMMs: Y += X W^T (+ b)
 };
 
 // Process-wide GEMM arithmetic (nrms_set_gemm_arith; defined in capi.hip).
