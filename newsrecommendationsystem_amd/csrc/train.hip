@@ -2,7 +2,8 @@
 // the autograd of src/model/NRMS (news_encoder.py:27-48, user_encoder.py:15-26,
 // multihead_self.py:15-75, additive.py:27-53, dot_product.py:8-19) and the
 // optimizer step of src/train.py:127,205-236, restated as explicit backward
-// kernels. fp32 throughout; the weight-gradient GEMM runs on f32 MFMA.
+// kernels. fp32 results; the weight-gradient GEMM runs on split-bf16 x6
+// (exact f32 MFMA under NRMS_GEMM=f32).
 //
 //   dropout            counter-based: keep(i) = hash(seed, i) >= p, so the
 //                      backward regenerates the mask instead of storing it
@@ -245,6 +246,120 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ 
   if (db && blockIdx.y == 0 && tid < TN_TILE && n0 + tid < N) atomicAdd(db + n0 + tid, bsum);
 }
 
+// The same dW += dY^T X on split-bf16 x6 (v_mfma_f32_16x16x32_bf16, the
+// forward GEMMs' arithmetic): per 32-row chunk each thread loads a 4 (rows) x
+// 4 (columns) block of dY (threads 0..127) or X (128..255), transposes it in
+// registers and stores each column's 4 rows as three bf16 planes, so LDS holds
+// [plane][n or k][32 rows] and every MFMA fragment (8 consecutive rows of one
+// column) is one conflict-free ds_read_b128 (64-B rows, chunk kq at kq ^ xsw).
+// db sums stay exact fp32, from the loaded registers.
+typedef __bf16 tn_bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ int tn_xsw(int row) { return ((row >> 3) & 1) << 1; }
+
+__global__ __launch_bounds__(256) void gemm_tn_x6_kernel(const float* __restrict__ dY, int64_t R,
+                                                         int N, const float* __restrict__ X, int K,
+                                                         float* __restrict__ dW,
+                                                         float* __restrict__ db) {
+  constexpr int RK = 32, PL = TN_TILE * RK;   // rows per chunk, bf16 per plane
+  __shared__ __attribute__((aligned(16))) __bf16 sa[3 * PL], sb[3 * PL];
+  const int n0 = blockIdx.x * TN_TILE, k0 = blockIdx.y * TN_TILE;
+  const int64_t r0 = (int64_t)blockIdx.z * TN_ROWS;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lm = lane & 15, kq = lane >> 4;
+  // staging role: a 4 x 4 block (rows 4 rb.., columns 4 cb..) of dY or X
+  const bool isa = tid < 128;
+  const int t = tid & 127, rb = t >> 4, cb = t & 15;
+  const float* src = isa ? dY : X;
+  const int ld = isa ? N : K;
+  const int c0 = (isa ? n0 : k0) + 4 * cb;
+  const bool cin = c0 < ld;   // ld % 4 == 0: a float4 is all in or all out
+  __bf16* dst = isa ? sa : sb;
+  float4 v[4];
+  auto gload = [&](int64_t rbase) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int64_t r = rbase + 4 * rb + i;
+      v[i] = (cin && r < R) ? *reinterpret_cast<const float4*>(src + r * ld + c0)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  float bs[4] = {0.f, 0.f, 0.f, 0.f};   // db partials of columns c0..c0+3
+  auto stage = [&]() {
+    const float col[4][4] = {{v[0].x, v[1].x, v[2].x, v[3].x}, {v[0].y, v[1].y, v[2].y, v[3].y},
+                             {v[0].z, v[1].z, v[2].z, v[3].z}, {v[0].w, v[1].w, v[2].w, v[3].w}};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (isa) bs[c] += ((col[c][0] + col[c][1]) + col[c][2]) + col[c][3];
+      uint32_t h0, m0, l0, h1, m1, l1;
+      split3x2(col[c][0], col[c][1], h0, m0, l0);
+      split3x2(col[c][2], col[c][3], h1, m1, l1);
+      const int row = 4 * cb + c;
+      __bf16* d = dst + row * RK + (((rb >> 1) ^ tn_xsw(row)) << 3) + (rb & 1) * 4;
+      *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+      *reinterpret_cast<uint2*>(d + PL) = make_uint2(m0, m1);
+      *reinterpret_cast<uint2*>(d + 2 * PL) = make_uint2(l0, l1);
+    }
+  };
+  floatx4 acc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int arow = 16 * w + lm;
+  const __bf16* Af = sa + arow * RK + ((kq ^ tn_xsw(arow)) << 3);
+  const __bf16* Bf = sb + lm * RK + ((kq ^ tn_xsw(lm)) << 3);   // + 16 j rows: same swizzle
+
+  gload(r0);
+  stage();
+  __syncthreads();
+  for (int rc = 0; rc < TN_ROWS; rc += RK) {
+    const bool more = rc + RK < TN_ROWS && r0 + rc + RK < R;
+    if (more) gload(r0 + rc + RK);
+    tn_bf16x8 a[3];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) a[pl] = *reinterpret_cast<const tn_bf16x8*>(Af + pl * PL);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      tn_bf16x8 b[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        b[pl] = *reinterpret_cast<const tn_bf16x8*>(Bf + pl * PL + 16 * j * RK);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[2], b[0], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[1], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[2], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[1], b[0], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[1], acc[j], 0, 0, 0);
+      acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[0], b[0], acc[j], 0, 0, 0);
+    }
+    if (!more) break;
+    __syncthreads();
+    stage();
+    __syncthreads();
+  }
+  // C/D: col = lane & 15 (k), row = 4 (lane >> 4) + reg (n)
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 16 * w + 4 * kq + r, k = k0 + 16 * j + lm;
+      if (n < N && k < K) atomicAdd(dW + (int64_t)n * K + k, acc[j][r]);
+    }
+  if (db && blockIdx.y == 0) {
+    // the slice's rows are spread over the 8 rb threads of a column block:
+    // combine their partials through LDS (the staging tiles are free now)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(sb);   // [8 rb][64 columns]
+    if (isa)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[rb * TN_TILE + 4 * cb + c] = bs[c];
+    __syncthreads();
+    if (tid < TN_TILE && n0 + tid < N) {
+      float sum = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sum += red[q * TN_TILE + tid];
+      atomicAdd(db + n0 + tid, sum);
+    }
+  }
+}
+
 // dtable[ids[t]] += dx[t] for ids[t] != padding_idx (nn.Embedding(padding_idx=0)
 // leaves that row's gradient zero). One wave per token row, 4 columns per lane.
 __global__ __launch_bounds__(256) void embedding_backward_kernel(
@@ -353,7 +468,12 @@ int32_t launch_gemm_tn(const float* dY, int64_t R, int N, const float* X, int K,
   const int64_t zs = (R + TN_ROWS - 1) / TN_ROWS;
   if (zs > 65535) return NRMS_ERR_UNSUPPORTED;
   dim3 grid((N + TN_TILE - 1) / TN_TILE, (K + TN_TILE - 1) / TN_TILE, (unsigned)zs);
-  hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, dW, db);
+  const bool x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6 && N % 4 == 0 && K % 4 == 0 &&
+                  ((uintptr_t)dY | (uintptr_t)X) % 16 == 0;
+  if (x6)
+    hipLaunchKernelGGL(gemm_tn_x6_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, dW, db);
+  else
+    hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, dW, db);
   return launch_status();
 }
 
