@@ -137,7 +137,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   // ---------------- 1. attention: thread = (head, query) ----------------
   float acc[UDK];
   if (has) {
-    const float rs = 1.0f / sqrtf((float)UDK);
+    // exp(d / sqrt(d_k)) as v_exp_f32(d · log2(e) / sqrt(d_k)), as the news kernel
+    const float rs = 1.4426950408889634f / sqrtf((float)UDK);
     // Keys j >= L read row L-1 and get weight 0 (no per-key branch, so the
     // independent dot products interleave); adding 0 changes no sum.
     auto raw = [&](int j) {
@@ -152,7 +153,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         d = fmaf(q[4 * t + 2], k4.z, d);
         d = fmaf(q[4 * t + 3], k4.w, d);
       }
-      return j < L ? expf(d * rs) : 0.f;
+      return j < L ? __builtin_amdgcn_exp2f(d * rs) : 0.f;
     };
     // LMAX = 64 would not fit the exps in registers at 16 waves: recompute
     // them in the second pass (expf is deterministic: same weights).
