@@ -22,6 +22,14 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
          "-Wall", "-Wno-unused-function"]
+# Per-file machine-scheduler strategy (measured in A/B runs on one box, bench
+# workload): the news kernel is 2.5 % faster under the iterative ILP
+# scheduler, the x6 projection GEMM 2 % faster under max-ILP; the other
+# strategies were no better than the default for either.
+FILE_FLAGS = {
+    "news_fused.hip": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+    "gemm_f32.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+}
 
 
 def _newer(src_paths, dst):
@@ -32,7 +40,8 @@ def _newer(src_paths, dst):
 
 
 def _deps():
-    return [os.path.join(CSRC, "nrms_common.hpp"), os.path.join(INCLUDE, "nrms_hip.h")]
+    return [os.path.join(CSRC, "nrms_common.hpp"), os.path.join(INCLUDE, "nrms_hip.h"),
+            os.path.abspath(__file__)]   # flag changes rebuild too
 
 
 def build(force=False, verbose=True):
@@ -46,7 +55,7 @@ def build(force=False, verbose=True):
 
     def compile_one(job):
         src, obj = job
-        cmd = [HIPCC] + FLAGS + ["-c", src, "-o", obj]
+        cmd = [HIPCC] + FLAGS + FILE_FLAGS.get(os.path.basename(src), []) + ["-c", src, "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
