@@ -194,6 +194,94 @@ __global__ __launch_bounds__(256) void mhsa_backward_kernel(const float* __restr
   }
 }
 
+// The same for titles (L <= 20) with one WAVE per (sequence, head): four
+// independent tasks per workgroup, each on its own LDS slice, phases
+// separated by wave-level LDS fences instead of workgroup barriers (the
+// workgroup version spends most of its time in five barriers around
+// 400-element loops).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__global__ __launch_bounds__(256) void mhsa_backward_wave_kernel(const float* __restrict__ qkv,
+                                                                 const float* __restrict__ dctx,
+                                                                 int64_t n_tasks, int L, int D,
+                                                                 int H, float* __restrict__ dqkv) {
+  constexpr int DK = 20, LM = 20;
+  struct Slice {
+    float q[LM][DK], k[LM][DK], v[LM][DK], o[LM][DK];
+    float a[LM][LM + 1], da[LM][LM + 1], row[LM];
+  };
+  __shared__ Slice ws[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int64_t task = (int64_t)blockIdx.x * 4 + wv;
+  if (task >= n_tasks) return;   // no workgroup barrier below: a finished wave may leave
+  const int64_t s = task / H;
+  const int h = (int)(task - s * H);
+  Slice& W = ws[wv];
+  const int ld = 3 * D;
+  const float rs = 1.0f / sqrtf((float)DK);
+  for (int e = lane; e < L * DK; e += 64) {
+    const int i = e / DK, t = e - i * DK;
+    const float* row = qkv + (s * L + i) * ld + h * DK + t;
+    W.q[i][t] = row[0];
+    W.k[i][t] = row[D];
+    W.v[i][t] = row[2 * D];
+    W.o[i][t] = dctx[(s * L + i) * D + h * DK + t];
+  }
+  wave_lds_sync();
+  for (int e = lane; e < L * L; e += 64) {
+    const int i = e / L, j = e - i * L;
+    float d = 0.f, g = 0.f;
+#pragma unroll
+    for (int t = 0; t < DK; ++t) {
+      d = fmaf(W.q[i][t], W.k[j][t], d);
+      g = fmaf(W.o[i][t], W.v[j][t], g);
+    }
+    W.a[i][j] = expf(d * rs);
+    W.da[i][j] = g;
+  }
+  wave_lds_sync();
+  if (lane < L) {
+    const int i = lane;
+    float z = 0.f;
+    for (int j = 0; j < L; ++j) z += W.a[i][j];
+    const float inv = 1.0f / (z + 1e-8f);
+    float rd = 0.f;
+    for (int j = 0; j < L; ++j) {
+      const float a = W.a[i][j] * inv;
+      W.a[i][j] = a;
+      rd = fmaf(W.da[i][j], a, rd);
+    }
+    W.row[i] = rd;
+  }
+  wave_lds_sync();
+  for (int e = lane; e < L * DK; e += 64) {
+    const int j = e / DK, t = e - j * DK;
+    float acc = 0.f;
+    for (int i = 0; i < L; ++i) acc = fmaf(W.a[i][j], W.o[i][t], acc);
+    dqkv[(s * L + j) * ld + 2 * D + h * DK + t] = acc;
+  }
+  wave_lds_sync();
+  for (int e = lane; e < L * L; e += 64) {
+    const int i = e / L, j = e - i * L;
+    W.da[i][j] = W.a[i][j] * (W.da[i][j] - W.row[i]) * rs;
+  }
+  wave_lds_sync();
+  for (int e = lane; e < L * DK; e += 64) {
+    const int i = e / DK, t = e - i * DK;
+    float gq = 0.f, gk = 0.f;
+    for (int j = 0; j < L; ++j) {
+      gq = fmaf(W.da[i][j], W.k[j][t], gq);
+      gk = fmaf(W.da[j][i], W.q[j][t], gk);
+    }
+    dqkv[(s * L + i) * ld + h * DK + t] = gq;
+    dqkv[(s * L + i) * ld + D + h * DK + t] = gk;
+  }
+}
+
 // dW[n][k] += sum_r dY[r][n] X[r][k] (+ db[n] += sum_r dY[r][n] from the
 // column tile 0 blocks). f32 MFMA 16x16x4; block = 64 (n) x 64 (k) tile over a
 // 256-row slice, 4 waves each a 16-row (n) strip x 64 cols; LDS tiles of
@@ -453,9 +541,9 @@ int32_t launch_mhsa_backward(const float* qkv, const float* dctx, int64_t n_seq,
   if (D != 20 * H || L < 1 || L > 64) return NRMS_ERR_UNSUPPORTED;
   const int64_t blocks = n_seq * H;
   if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
-  if (L <= 20)
-    hipLaunchKernelGGL(mhsa_backward_kernel<20>, dim3((unsigned)blocks), dim3(256), 0, s, qkv, dctx,
-                       L, D, H, dqkv);
+  if (L <= 20)   // titles: one wave per (title, head); 297 -> 311 training steps/s
+    hipLaunchKernelGGL(mhsa_backward_wave_kernel, dim3((unsigned)((blocks + 3) / 4)), dim3(256), 0,
+                       s, qkv, dctx, blocks, L, D, H, dqkv);
   else
     hipLaunchKernelGGL(mhsa_backward_kernel<64>, dim3((unsigned)blocks), dim3(256), 0, s, qkv, dctx,
                        L, D, H, dqkv);
