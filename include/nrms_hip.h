@@ -280,6 +280,24 @@ int32_t nrms_adam_step(float* param, const float* grad, float* exp_avg, float* e
                        int64_t n, float lr, float beta1, float beta2, float eps, int64_t step,
                        hipStream_t stream);
 
+/* The same Adam step over many parameters in ONE launch. `tensors` is a
+ * DEVICE array of n descriptors; tensor i owns the ceil(numel / 256) thread
+ * blocks starting at first_block (the caller's prefix sum, total_blocks in
+ * all). All tensors share lr / betas / eps / step. Replaces one
+ * nrms_adam_step launch per parameter (torch.optim.Adam's foreach path). */
+typedef struct {
+  float* param;
+  const float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  int64_t numel;
+  int64_t first_block;
+} nrms_adam_tensor_t;
+
+int32_t nrms_adam_step_multi(const nrms_adam_tensor_t* tensors, int32_t n, int64_t total_blocks,
+                             float lr, float beta1, float beta2, float eps, int64_t step,
+                             hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

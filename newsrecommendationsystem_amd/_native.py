@@ -72,6 +72,8 @@ SIGNATURES = {
     "nrms_embedding_backward": (_i32, [_p, _i64, _p, _i64, _i32, _i64, _p, _p]),
     "nrms_adam_step": (_i32, [_p, _p, _p, _p, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, _i64, _p]),
+    "nrms_adam_step_multi": (_i32, [_p, _i32, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                    ctypes.c_float, _i64, _p]),
     "nrms_forward_workspace_size": (_sz, [_i64, _i32, _i32, _i32, _i64, _i32, _i32]),
     "nrms_forward": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _p, _i64, _EW, _EW, _i32, _p, _p,
                             _sz, _p]),

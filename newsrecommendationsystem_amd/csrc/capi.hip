@@ -528,4 +528,12 @@ int32_t nrms_adam_step(float* param, const float* grad, float* exp_avg, float* e
   return launch_adam(param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, step, stream);
 }
 
+int32_t nrms_adam_step_multi(const nrms_adam_tensor_t* tensors, int32_t n, int64_t total_blocks,
+                             float lr, float beta1, float beta2, float eps, int64_t step,
+                             hipStream_t stream) {
+  if (n < 0 || total_blocks < 0 || step < 1) return NRMS_ERR_INVALID_ARG;
+  if (n > 0 && !tensors) return NRMS_ERR_INVALID_ARG;
+  return launch_adam_multi(tensors, n, total_blocks, lr, beta1, beta2, eps, step, stream);
+}
+
 }  // extern "C"

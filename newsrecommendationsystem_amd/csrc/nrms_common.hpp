@@ -129,6 +129,8 @@ int32_t launch_transpose(const float* const* src, int nseg, int seg_rows, int co
                          hipStream_t s);
 int32_t launch_embedding_backward(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
                                   int D, int64_t padding_idx, float* dtable, hipStream_t s);
+int32_t launch_adam_multi(const nrms_adam_tensor_t* ts, int n, int64_t total_blocks, float lr,
+                          float b1, float b2, float eps, int64_t step, hipStream_t s);
 int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                     float b2, float eps, int64_t step, hipStream_t s);
 

@@ -480,6 +480,26 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
   p[i] -= (lr / bc1) * (mi / denom);
 }
 
+// Multi-tensor Adam: block b belongs to the tensor whose [first_block,
+// next first_block) range holds it (n is small: a linear scan).
+__global__ __launch_bounds__(256) void adam_multi_kernel(const nrms_adam_tensor_t* __restrict__ ts,
+                                                         int n, float lr, float b1, float b2,
+                                                         float eps, float bc1, float bc2_sqrt) {
+  const int64_t b = blockIdx.x;
+  int t = 0;
+  while (t + 1 < n && ts[t + 1].first_block <= b) ++t;
+  const nrms_adam_tensor_t d = ts[t];
+  const int64_t i = (b - d.first_block) * 256 + threadIdx.x;
+  if (i >= d.numel) return;
+  const float gi = d.grad[i];
+  const float mi = d.exp_avg[i] + (1.0f - b1) * (gi - d.exp_avg[i]);
+  const float vi = d.exp_avg_sq[i] * b2 + (1.0f - b2) * gi * gi;
+  d.exp_avg[i] = mi;
+  d.exp_avg_sq[i] = vi;
+  const float denom = sqrtf(vi) / bc2_sqrt + eps;
+  d.param[i] -= (lr / bc1) * (mi / denom);
+}
+
 // dst[c][r] = W[r][c] for the stacked segments W = [src_0; src_1; ...]
 // (seg_rows rows each, `cols` columns): the [in, out] copy of nn.Linear
 // weights that turns dX = dY W into the X W^T form of the store GEMM.
@@ -580,6 +600,17 @@ int32_t launch_embedding_backward(const int64_t* ids, int64_t n_tok, const float
   if (n_tok == 0) return NRMS_OK;
   hipLaunchKernelGGL(embedding_backward_kernel, dim3((unsigned)((n_tok + 3) / 4)), dim3(256), 0, s,
                      ids, n_tok, dx, V, D, padding_idx, dtable);
+  return launch_status();
+}
+
+int32_t launch_adam_multi(const nrms_adam_tensor_t* ts, int n, int64_t total_blocks, float lr,
+                          float b1, float b2, float eps, int64_t step, hipStream_t s) {
+  if (n == 0 || total_blocks == 0) return NRMS_OK;
+  if (total_blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  const float bc1 = (float)(1.0 - pow((double)b1, (double)step));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, (double)step));
+  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)total_blocks), dim3(256), 0, s, ts, n, lr, b1,
+                     b2, eps, bc1, bc2_sqrt);
   return launch_status();
 }
 

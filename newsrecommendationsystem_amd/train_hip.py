@@ -24,7 +24,9 @@ HipAdam is torch.optim.Adam's update on the same state keys (exp_avg,
 exp_avg_sq, step), so optimizer state_dicts interchange with the reference's.
 """
 import ctypes
+import os
 
+import numpy as np
 import torch
 
 from . import _native as N
@@ -189,17 +191,26 @@ def forward_hip(model, cand_ids, clicked_ids, seed):
 
 
 class HipAdam(torch.optim.Optimizer):
-    """torch.optim.Adam (amsgrad=False, weight_decay=0, maximize=False) with the
-    update as one nrms_adam_step launch per parameter; same state keys."""
+    """torch.optim.Adam (amsgrad=False, weight_decay=0, maximize=False) on the
+    HIP update kernel; same state keys. A parameter group whose parameters all
+    have gradients and the same step count is updated in ONE
+    nrms_adam_step_multi launch (a device table of per-tensor descriptors);
+    otherwise one nrms_adam_step launch per parameter."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
+        # per group: (descriptor rows, device table, pinned staging copy, copy event).
+        # The table is rebuilt only when a pointer changes (gradients set to None
+        # and re-allocated usually come back at the same addresses).
+        self._tables = {}
+        self._multi = os.environ.get("NRMS_ADAM_PER_PARAM") is None
 
     @torch.no_grad()
     def step(self, closure=None):
         loss = closure() if closure is not None else None
-        for group in self.param_groups:
+        for gi, group in enumerate(self.param_groups):
             b1, b2 = group["betas"]
+            live = []
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -210,8 +221,37 @@ class HipAdam(torch.optim.Optimizer):
                     state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 state["step"] += 1
                 g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                N.call("nrms_adam_step", N.ptr(p), N.ptr(g), N.ptr(state["exp_avg"]),
-                       N.ptr(state["exp_avg_sq"]), p.numel(), ctypes.c_float(group["lr"]),
-                       ctypes.c_float(b1), ctypes.c_float(b2), ctypes.c_float(group["eps"]),
-                       int(state["step"].item()), N.stream_handle(p.device))
+                live.append((p, g, state))
+            if not live:
+                continue
+            steps = {int(st["step"].item()) for _, _, st in live}
+            args = (ctypes.c_float(group["lr"]), ctypes.c_float(b1), ctypes.c_float(b2),
+                    ctypes.c_float(group["eps"]))
+            dev = live[0][0].device
+            if self._multi and len(steps) == 1 and all(p.device == dev for p, _, _ in live):
+                rows, first = [], 0
+                for p, g, st in live:
+                    n = p.numel()
+                    rows.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                                 st["exp_avg_sq"].data_ptr(), n, first))
+                    first += (n + 255) // 256
+                rows = tuple(rows)
+                ent = self._tables.get(gi)
+                if ent is None or ent[0] != rows:
+                    if ent is not None:
+                        ent[3].synchronize()   # the old staging copy has been consumed
+                    pinned = torch.from_numpy(np.array(rows, dtype=np.int64)).pin_memory()
+                    table = torch.empty(pinned.shape, dtype=torch.int64, device=dev)
+                    table.copy_(pinned, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    ent = (rows, table, pinned, ev)
+                    self._tables[gi] = ent
+                N.call("nrms_adam_step_multi", N.ptr(ent[1]), len(live), first, *args,
+                       steps.pop(), N.stream_handle(dev))
+            else:
+                for p, g, st in live:
+                    N.call("nrms_adam_step", N.ptr(p), N.ptr(g), N.ptr(st["exp_avg"]),
+                           N.ptr(st["exp_avg_sq"]), p.numel(), *args, int(st["step"].item()),
+                           N.stream_handle(p.device))
         return loss
