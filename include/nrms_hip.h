@@ -11,9 +11,14 @@
  *
  * Conventions
  *   - All tensor arguments are caller-allocated DEVICE pointers, borrowed for
- *     the call. The library never allocates or frees, never synchronises the
- *     stream, and keeps no state: any host thread may call it on any stream,
- *     and every call is capturable into a hipGraph.
+ *     the call (except nrms_adam_step_multi's descriptor array, a HOST array
+ *     read during the call). The library never allocates or frees device
+ *     memory and never synchronises the stream; any host thread may call it
+ *     on any stream, and every call is capturable into a hipGraph. It keeps
+ *     no per-call state. Process-wide state is limited to: the GEMM
+ *     arithmetic (nrms_set_gemm_arith, an atomic read at enqueue time), the
+ *     last HIP error (thread-local), and a mutex-guarded record of which
+ *     (device, kernel) pairs have had their dynamic-LDS limit raised.
  *   - fp32 row-major everywhere; ids are int64 (the reference's LongTensor).
  *   - Every function returns NRMS_OK (0) or an nrms_status_t error code; a
  *     launch failure returns NRMS_ERR_HIP and the HIP error is kept for
@@ -36,7 +41,9 @@
 extern "C" {
 #endif
 
-#define NRMS_ABI_VERSION 1
+/* 2: nrms_user_encode takes batch / row strides; nrms_adam_step_multi takes a
+ *    host descriptor array (no device table, no total_blocks). */
+#define NRMS_ABI_VERSION 2
 
 typedef enum {
   NRMS_OK = 0,
@@ -159,12 +166,17 @@ int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
                                 const nrms_encoder_weights_t* w, float* out,
                                 void* workspace, size_t workspace_bytes, hipStream_t stream);
 
-/* UserEncoder.forward (src/model/NRMS/user_encoder.py:15-26): clicked[B, N, D]
- * (row-major, contiguous) -> out[B, D]. */
+/* UserEncoder.forward (src/model/NRMS/user_encoder.py:15-26), also
+ * NRMS.get_user_vector (src/model/NRMS/__init__.py:63-71): clicked is a
+ * [B, N, D] view, element (b, n, d) at clicked[b*stride_b + n*stride_n + d]
+ * (strides in floats, multiples of 4; the innermost stride is 1) -> out[B, D].
+ * Contiguous input: stride_b = N*D, stride_n = D. The reference caller's
+ * torch.stack(..., dim=0).transpose(0, 1) view (src/evaluate.py:220-224) is
+ * stride_b = D, stride_n = B*D and is read in place, without a copy. */
 size_t nrms_user_encode_workspace_size(int64_t B, int32_t N, int32_t D);
-int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N,
-                         const nrms_encoder_weights_t* w, float* out, void* workspace,
-                         size_t workspace_bytes, hipStream_t stream);
+int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N, int64_t stride_b,
+                         int64_t stride_n, const nrms_encoder_weights_t* w, float* out,
+                         void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Fused UserEncoder tail (user_encoder.py:15-26 after the projection): raw-exp
  * MHSA over qkv[B*N, 3D] (row b*N + i) + additive attention + pooling, one
@@ -194,9 +206,11 @@ int32_t nrms_score_pairs(const float* news, int64_t n_news, const float* user, i
 
 /* Per-impression ranking metrics (src/evaluate.py:24-42,160-168) over ragged
  * impressions: impression i owns scores/labels [offsets[i], offsets[i+1]).
- * out[i*4 + {0,1,2,3}] = AUC, MRR, nDCG@5, nDCG@10 in fp64; all four NaN when
- * the impression has one class only or a NaN score (the reference's
- * ValueError branch). Ranking order = np.argsort(score)[::-1]: descending,
+ * out[i*4 + {0,1,2,3}] = AUC, MRR, nDCG@5, nDCG@10 in fp64. A non-finite
+ * score or an empty impression: all four NaN (roc_auc_score raises, the
+ * reference's ValueError branch). One class only: AUC NaN (scikit-learn >= 1.3
+ * warns instead of raising) and MRR / nDCG as numpy computes them (all
+ * negative: NaN; all positive: MRR = mean(1/rank), nDCG = 1). Ranking order = np.argsort(score)[::-1]: descending,
  * equal scores by larger index first. */
 int32_t nrms_impression_metrics(const float* scores, const int32_t* labels,
                                 const int64_t* offsets, int64_t n_imp, double* out,
@@ -280,11 +294,12 @@ int32_t nrms_adam_step(float* param, const float* grad, float* exp_avg, float* e
                        int64_t n, float lr, float beta1, float beta2, float eps, int64_t step,
                        hipStream_t stream);
 
-/* The same Adam step over many parameters in ONE launch. `tensors` is a
- * DEVICE array of n descriptors; tensor i owns the ceil(numel / 256) thread
- * blocks starting at first_block (the caller's prefix sum, total_blocks in
- * all). All tensors share lr / betas / eps / step. Replaces one
- * nrms_adam_step launch per parameter (torch.optim.Adam's foreach path). */
+/* The same Adam step over many parameters: `tensors` is a HOST array of n
+ * descriptors, read during the call; up to 32 of them go to the device by
+ * value in the kernel arguments of one launch (ceil(n / 32) launches). All
+ * tensors share lr / betas / eps / step. Replaces one nrms_adam_step launch
+ * per parameter (torch.optim.Adam's foreach path). `first_block` is ignored
+ * (kept for layout stability). */
 typedef struct {
   float* param;
   const float* grad;
@@ -294,9 +309,8 @@ typedef struct {
   int64_t first_block;
 } nrms_adam_tensor_t;
 
-int32_t nrms_adam_step_multi(const nrms_adam_tensor_t* tensors, int32_t n, int64_t total_blocks,
-                             float lr, float beta1, float beta2, float eps, int64_t step,
-                             hipStream_t stream);
+int32_t nrms_adam_step_multi(const nrms_adam_tensor_t* tensors, int32_t n, float lr, float beta1,
+                             float beta2, float eps, int64_t step, hipStream_t stream);
 
 #ifdef __cplusplus
 }

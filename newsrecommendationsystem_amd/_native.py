@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NRMS_LIB_PATH") or os.path.join(_PKG, "libnrms_hip.so")   # override: A/B builds
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
 NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32 = 0, 1
@@ -56,7 +56,7 @@ SIGNATURES = {
     "nrms_user_attention_pool_workspace_size": (_sz, [_i64, _i32, _i32]),
     "nrms_user_attention_pool": (_i32, [_p, _i64, _i32, _EW, _p, _p, _sz, _p]),
     "nrms_user_encode_workspace_size": (_sz, [_i64, _i32, _i32]),
-    "nrms_user_encode": (_i32, [_p, _i64, _i32, _EW, _p, _p, _sz, _p]),
+    "nrms_user_encode": (_i32, [_p, _i64, _i32, _i64, _i64, _EW, _p, _p, _sz, _p]),
     "nrms_score": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p]),
     "nrms_score_pairs": (_i32, [_p, _i64, _p, _i64, _p, _p, _i64, _i32, _p, _p]),
     "nrms_impression_metrics": (_i32, [_p, _p, _p, _i64, _p, _p]),
@@ -72,7 +72,7 @@ SIGNATURES = {
     "nrms_embedding_backward": (_i32, [_p, _i64, _p, _i64, _i32, _i64, _p, _p]),
     "nrms_adam_step": (_i32, [_p, _p, _p, _p, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, _i64, _p]),
-    "nrms_adam_step_multi": (_i32, [_p, _i32, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
+    "nrms_adam_step_multi": (_i32, [_p, _i32, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                                     ctypes.c_float, _i64, _p]),
     "nrms_forward_workspace_size": (_sz, [_i64, _i32, _i32, _i32, _i64, _i32, _i32]),
     "nrms_forward": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _p, _i64, _EW, _EW, _i32, _p, _p,

@@ -19,7 +19,6 @@
 // the weighted sum of the token rows. One wave per sequence.
 #include "nrms_common.hpp"
 
-#include <mutex>
 
 namespace nrms {
 namespace {
@@ -53,8 +52,9 @@ __global__ __launch_bounds__(NT) void mhsa_rawexp_kernel(
   }
   __syncthreads();
 
-  // 1/sqrt(d_k) in fp32; the reference divides by np.sqrt(d_k) (1-ulp apart).
-  const float rs = 1.0f / sqrtf((float)DK);
+  // fast path exp2(d * log2(e) / sqrt(d_k)); exact path for rows near overflow
+  const float c_exp = 1.4426950408889634f / sqrtf((float)DK);
+  const float sqrt_dk = sqrtf((float)DK);
   for (int task = tid; task < L * H; task += NT) {
     const int h = task / L;
     const int i = task - h * L;
@@ -73,25 +73,32 @@ __global__ __launch_bounds__(NT) void mhsa_rawexp_kernel(
       for (int t = 0; t < DK; ++t) q[t] = qnan();
     }
 
+    auto dot = [&](int j) {
+      const float4* kr = reinterpret_cast<const float4*>(kv + (size_t)j * 2 * D + h * DK);
+      float d = 0.f;
+#pragma unroll
+      for (int t = 0; t < DK / 4; ++t) {
+        const float4 k4 = kr[t];
+        d = fmaf(q[4 * t], k4.x, d);
+        d = fmaf(q[4 * t + 1], k4.y, d);
+        d = fmaf(q[4 * t + 2], k4.z, d);
+        d = fmaf(q[4 * t + 3], k4.w, d);
+      }
+      return d;
+    };
     float e[LMAX];
     float sum = 0.f;
 #pragma unroll
     for (int j = 0; j < LMAX; ++j) {
-      if (j < L) {
-        const float4* kr = reinterpret_cast<const float4*>(kv + (size_t)j * 2 * D + h * DK);
-        float d = 0.f;
+      e[j] = j < L ? __builtin_amdgcn_exp2f(dot(j) * c_exp) : 0.f;
+      sum += e[j];
+    }
+    if (exp_row_needs_recheck(sum)) {   // rare: rows near fp32 overflow (nrms_common.hpp)
+      sum = 0.f;
 #pragma unroll
-        for (int t = 0; t < DK / 4; ++t) {
-          const float4 k4 = kr[t];
-          d = fmaf(q[4 * t], k4.x, d);
-          d = fmaf(q[4 * t + 1], k4.y, d);
-          d = fmaf(q[4 * t + 2], k4.z, d);
-          d = fmaf(q[4 * t + 3], k4.w, d);
-        }
-        e[j] = expf(d * rs);
+      for (int j = 0; j < LMAX; ++j) {
+        e[j] = j < L ? ref_exp(dot(j), sqrt_dk) : 0.f;
         sum += e[j];
-      } else {
-        e[j] = 0.f;
       }
     }
     const float inv = 1.0f / (sum + 1e-8f);
@@ -141,7 +148,8 @@ __global__ __launch_bounds__(kLongThreads) void mhsa_rawexp_long_kernel(
     lrow[i] = ((uint64_t)r < (uint64_t)n_rows) ? r : -1;
   }
   __syncthreads();
-  const float rs = 1.0f / sqrtf((float)DK);
+  const float c_exp = 1.4426950408889634f / sqrtf((float)DK);
+  const float sqrt_dk = sqrtf((float)DK);
   for (int task = tid; task < L * H; task += kLongThreads) {
     const int h = task / L;
     const int i = task - h * L;
@@ -152,6 +160,7 @@ __global__ __launch_bounds__(kLongThreads) void mhsa_rawexp_long_kernel(
       const float4 v = r >= 0 ? reinterpret_cast<const float4*>(qkv + r * ld + h * DK)[t] : nan4();
       q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
     }
+    bool exact = false;   // the row takes the reference's exp (kExpRecheck)
     auto raw = [&](int j) {
       const int64_t rj = lrow[j];
       float d = 0.f;
@@ -164,10 +173,15 @@ __global__ __launch_bounds__(kLongThreads) void mhsa_rawexp_long_kernel(
         d = fmaf(q[4 * t + 2], k4.z, d);
         d = fmaf(q[4 * t + 3], k4.w, d);
       }
-      return expf(d * rs);
+      return exact ? ref_exp(d, sqrt_dk) : __builtin_amdgcn_exp2f(d * c_exp);
     };
     float sum = 0.f;
     for (int j = 0; j < L; ++j) sum += raw(j);
+    if (exp_row_needs_recheck(sum)) {
+      exact = true;
+      sum = 0.f;
+      for (int j = 0; j < L; ++j) sum += raw(j);
+    }
     const float inv = 1.0f / (sum + 1e-8f);
     float acc[DK];
 #pragma unroll
@@ -257,11 +271,8 @@ int32_t launch_mhsa_inst(const float* qkv, int64_t n_rows, const int64_t* ids_a,
   constexpr int D = H * DK;
   const size_t lds = (size_t)L * 2 * D * sizeof(float) + (size_t)L * sizeof(int64_t);
   if (lds > 160 * 1024) return NRMS_ERR_UNSUPPORTED;
-  static std::once_flag once;
-  std::call_once(once, [] {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&mhsa_rawexp_kernel<LMAX, DK, H, NT>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  });
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&mhsa_rawexp_kernel<LMAX, DK, H, NT>),
+                     160 * 1024);
   hipLaunchKernelGGL((mhsa_rawexp_kernel<LMAX, DK, H, NT>), dim3((unsigned)n_seq), dim3(NT), lds,
                      s, qkv, n_rows, ids_a, n_seq_a, ids_b, L, ctx);
   return launch_status();

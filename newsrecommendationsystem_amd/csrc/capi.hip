@@ -1,10 +1,14 @@
 // C ABI (include/nrms_hip.h): argument validation, workspace carving and the
-// stage order of the NRMS encoders. Stateless; every call only enqueues work
-// on the caller's stream (no allocation, no synchronisation).
+// stage order of the NRMS encoders. Every call only enqueues work on the
+// caller's stream (no allocation, no synchronisation); the only globals are the
+// process-wide GEMM arithmetic and the once-per-(device, kernel) LDS attribute.
 #include "nrms_common.hpp"
 
 #include <atomic>
 #include <cstdlib>
+#include <mutex>
+#include <set>
+#include <tuple>
 
 namespace nrms {
 
@@ -17,6 +21,16 @@ static int initial_gemm_arith() {
 }
 static std::atomic<int> g_gemm_arith{initial_gemm_arith()};
 int gemm_arith() { return g_gemm_arith.load(std::memory_order_relaxed); }
+
+void ensure_dynamic_lds(const void* fn, int bytes) {
+  static std::mutex mu;
+  static std::set<std::tuple<int, const void*, int>> done;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> lock(mu);
+  if (done.insert(std::make_tuple(dev, fn, bytes)).second)
+    (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
 
 namespace {
 
@@ -77,7 +91,7 @@ struct NewsSizes {
 NewsSizes news_sizes(int64_t n_titles, int32_t L, int64_t V, int32_t D, bool folded) {
   const size_t ntok = (size_t)n_titles * (size_t)L;
   return {(folded ? (size_t)V : ntok) * 3 * (size_t)D, ntok * (size_t)D, ntok,
-          fused_news_packed_b_floats()};
+          fused_news_workspace_floats(n_titles)};
 }
 size_t news_bytes(const NewsSizes& z) {
   return align_up(z.qkv * 4) + align_up(z.ctx * 4) + align_up(z.scores * 4) + align_up(z.wap * 4);
@@ -187,7 +201,7 @@ int32_t nrms_additive_pool(const float* x, const float* scores, int64_t n_seq, i
 
 size_t nrms_news_attention_pool_workspace_size(int64_t n_titles, int32_t L, int32_t D) {
   if (n_titles < 0 || L <= 0 || D <= 0) return 0;
-  return align_up(fused_news_packed_b_floats() * 4);   // the context stays on chip
+  return align_up(fused_news_workspace_floats(n_titles) * 4);   // the context stays on chip
 }
 
 int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
@@ -200,7 +214,7 @@ int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int
   if (n_titles == 0) return NRMS_OK;
   if (!qkv || !out) return NRMS_ERR_INVALID_ARG;
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
-  float* wap = cv.floats(fused_news_packed_b_floats());
+  float* wap = cv.floats(fused_news_workspace_floats(n_titles));
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   return launch_fused_news(qkv, n_rows_qkv, tok_ids, n_seq_a, tok_ids_b, n_titles, w->w_add,
                            w->b_add, w->q_add, wap, out, stream);
@@ -247,7 +261,8 @@ int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const 
 size_t nrms_news_encode_folded_workspace_size(int64_t n_titles, int32_t L, int32_t D) {
   if (n_titles < 0 || L <= 0 || D <= 0) return 0;
   const size_t ntok = (size_t)n_titles * L;
-  return align_up(ntok * D * 4) + align_up(ntok * 4) + align_up(fused_news_packed_b_floats() * 4);
+  return align_up(ntok * D * 4) + align_up(ntok * 4) +
+         align_up(fused_news_workspace_floats(n_titles) * 4);
 }
 
 int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
@@ -262,7 +277,7 @@ int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
   float* ctx = cv.floats(ntok * w->d_model);
   float* scores = cv.floats(ntok);
-  float* wap = cv.floats(fused_news_packed_b_floats());
+  float* wap = cv.floats(fused_news_workspace_floats(n_titles));
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   return encode_from_qkv(qkv_table, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
                          stream, wap);
@@ -294,10 +309,10 @@ int32_t nrms_user_attention_pool(const float* qkv, int64_t B, int32_t N,
   return launch_fused_user(qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
 }
 
-int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N,
-                         const nrms_encoder_weights_t* w, float* out, void* workspace,
-                         size_t workspace_bytes, hipStream_t stream) {
-  if (B < 0 || N <= 0) return NRMS_ERR_INVALID_ARG;
+int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N, int64_t stride_b,
+                         int64_t stride_n, const nrms_encoder_weights_t* w, float* out,
+                         void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  if (B < 0 || N <= 0 || stride_b < 0 || stride_n < 0) return NRMS_ERR_INVALID_ARG;
   if (int32_t st = shape_ok(w)) return st;
   if (B == 0) return NRMS_OK;
   if (!clicked || !out) return NRMS_ERR_INVALID_ARG;
@@ -309,8 +324,12 @@ int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N,
   float* scores = cv.floats((size_t)rows);
   float* wap = cv.floats(fused_user_packed_b_floats());
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
-  int32_t st = launch_gemm_store(clicked, rows, nullptr, rows, D, qkv_rows(w), 3 * D, qkv, 3 * D,
-                                 stream);
+  // the [B, N, D] view is read in place (e.g. the transpose(0, 1) of
+  // src/evaluate.py:220-224: stride_b = D, stride_n = B * D)
+  const ARows ar = (stride_b == (int64_t)N * D && stride_n == D) ? contiguous_rows(D)
+                                                                 : ARows{N, stride_b, stride_n};
+  int32_t st = launch_gemm_store_rows(clicked, rows, ar, nullptr, rows, D, qkv_rows(w), 3 * D, qkv,
+                                      3 * D, stream);
   if (st) return st;
   if (fused_user_supported(N, D, w->n_heads, w->query_dim) && ((uintptr_t)out % 16) == 0)
     return launch_fused_user(qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
@@ -393,7 +412,7 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
                          news, stream, wap);
   }
   if (st) return st;
-  st = nrms_user_encode(news, B, N, user_w, user, user_ws, user_ws_bytes, stream);
+  st = nrms_user_encode(news, B, N, (int64_t)N * D, D, user_w, user, user_ws, user_ws_bytes, stream);
   if (st) return st;
   return launch_score(news + (size_t)n_clk * D, B, C, (int64_t)C * D, D, user, D, D, logits,
                       stream);
@@ -528,12 +547,17 @@ int32_t nrms_adam_step(float* param, const float* grad, float* exp_avg, float* e
   return launch_adam(param, grad, exp_avg, exp_avg_sq, n, lr, beta1, beta2, eps, step, stream);
 }
 
-int32_t nrms_adam_step_multi(const nrms_adam_tensor_t* tensors, int32_t n, int64_t total_blocks,
-                             float lr, float beta1, float beta2, float eps, int64_t step,
-                             hipStream_t stream) {
-  if (n < 0 || total_blocks < 0 || step < 1) return NRMS_ERR_INVALID_ARG;
+int32_t nrms_adam_step_multi(const nrms_adam_tensor_t* tensors, int32_t n, float lr, float beta1,
+                             float beta2, float eps, int64_t step, hipStream_t stream) {
+  if (n < 0 || step < 1) return NRMS_ERR_INVALID_ARG;
   if (n > 0 && !tensors) return NRMS_ERR_INVALID_ARG;
-  return launch_adam_multi(tensors, n, total_blocks, lr, beta1, beta2, eps, step, stream);
+  for (int32_t i = 0; i < n; ++i) {
+    const nrms_adam_tensor_t& t = tensors[i];
+    if (t.numel < 0) return NRMS_ERR_INVALID_ARG;
+    if (t.numel > 0 && (!t.param || !t.grad || !t.exp_avg || !t.exp_avg_sq))
+      return NRMS_ERR_INVALID_ARG;
+  }
+  return launch_adam_multi(tensors, n, lr, beta1, beta2, eps, step, stream);
 }
 
 }  // extern "C"

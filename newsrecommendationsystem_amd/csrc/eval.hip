@@ -6,9 +6,13 @@
 //  * per-impression ranking metrics (evaluate.py:24-42,160-168): AUC (the
 //    Mann-Whitney statistic with ties counted 1/2, which is what
 //    sklearn.metrics.roc_auc_score computes for binary labels), MRR, nDCG@5,
-//    nDCG@10, one wave per impression, fp64 accumulation; an impression with
-//    a single class (or a NaN score) gets NaN for all four, as the
-//    reference's ValueError branch does (evaluate.py:167-168).
+//    nDCG@10, one wave per impression, fp64 accumulation. Edge cases follow
+//    the reference as it runs against scikit-learn 1.7 (pinned by
+//    tests/golden/nrms_flow_golden.npz): a non-finite score makes
+//    roc_auc_score raise, so all four are NaN (the ValueError branch,
+//    evaluate.py:167-168); a single-class impression gets AUC = NaN (sklearn
+//    warns instead of raising) while MRR / nDCG keep numpy's arithmetic:
+//    all-negative -> 0/0 = NaN, all-positive -> MRR = mean(1/rank), nDCG = 1.
 #include "nrms_common.hpp"
 
 namespace nrms {
@@ -68,17 +72,17 @@ __global__ __launch_bounds__(kThreads) void impression_metrics_kernel(
   const float* s = scores + b;
   const int32_t* y = labels + b;
 
-  // class counts and NaN check
-  double npos = 0.0, nnan = 0.0;
+  // class counts and non-finite check (sklearn's check_array rejects NaN / inf)
+  double npos = 0.0, nbad = 0.0;
   for (int c = lane; c < n; c += kWave) {
     npos += (y[c] == 1) ? 1.0 : 0.0;
-    nnan += (s[c] != s[c]) ? 1.0 : 0.0;
+    nbad += __builtin_isfinite(s[c]) ? 0.0 : 1.0;
   }
   npos = wave_sum_d(npos);
-  nnan = wave_sum_d(nnan);
+  nbad = wave_sum_d(nbad);
   const double nneg = (double)n - npos;
   double* o = out + imp * 4;
-  if (n == 0 || npos == 0.0 || nneg == 0.0 || nnan > 0.0) {
+  if (n == 0 || npos == 0.0 || nbad > 0.0) {   // all-negative: every metric is 0/0
     if (lane < 4) o[lane] = __builtin_nan("");
     return;
   }
@@ -113,10 +117,11 @@ __global__ __launch_bounds__(kThreads) void impression_metrics_kernel(
     idcg10 += d;
   }
   if (lane == 0) {
-    o[0] = auc_num / (npos * nneg);
+    const bool one_class = nneg == 0.0;   // all positive: identical DCG arrays, ratio 1
+    o[0] = one_class ? __builtin_nan("") : auc_num / (npos * nneg);
     o[1] = rr / npos;
-    o[2] = dcg5 / idcg5;
-    o[3] = dcg10 / idcg10;
+    o[2] = one_class ? 1.0 : dcg5 / idcg5;
+    o[3] = one_class ? 1.0 : dcg10 / idcg10;
   }
 }
 

@@ -28,7 +28,7 @@ constexpr int kThreads = 256;
 // tiles (declared once by the kernel so both tile widths share them).
 template <int TN, bool ADDITIVE>
 __device__ __forceinline__ void gemm_tile(
-    const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
+    const float* __restrict__ X, int64_t n_rows_x, ARows ar, const int64_t* __restrict__ row_ids,
     int64_t M, int K, const WeightRows& wr, int N, float* __restrict__ Y, int64_t ldy,
     const float* __restrict__ qvec, float* __restrict__ score, int64_t m0, int n0,
     float* __restrict__ As, float* __restrict__ Bs) {
@@ -50,7 +50,7 @@ __device__ __forceinline__ void gemm_tile(
     a_bad[p] = false;
     if (m < M) {
       const int64_t r = row_ids ? row_ids[m] : m;
-      if ((uint64_t)r < (uint64_t)n_rows_x) a_src[p] = X + r * K;
+      if ((uint64_t)r < (uint64_t)n_rows_x) a_src[p] = X + ar.offset(r);
       else a_bad[p] = true;  // invalid id: the row becomes NaN
     }
   }
@@ -195,7 +195,7 @@ __device__ __forceinline__ void gemm_tile(
 // spent on all-padding columns.
 template <int TN, int TNT, bool ADDITIVE>
 __global__ __launch_bounds__(kThreads, 2) void gemm_xwt_f32_kernel(
-    const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
+    const float* __restrict__ X, int64_t n_rows_x, ARows ar, const int64_t* __restrict__ row_ids,
     int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy,
     const float* __restrict__ qvec, float* __restrict__ score, int n_col_tiles) {
   __shared__ __attribute__((aligned(16))) float As[BM * LDS_LD];
@@ -205,9 +205,9 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_xwt_f32_kernel(
   const int64_t m0 = (int64_t)(wg / n_col_tiles) * BM;
   const int n0 = ct * 16 * TN;
   if (TNT == TN || n0 + 16 * TN <= N)
-    gemm_tile<TN, ADDITIVE>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, qvec, score, m0, n0, As, Bs);
+    gemm_tile<TN, ADDITIVE>(X, n_rows_x, ar, row_ids, M, K, wr, N, Y, ldy, qvec, score, m0, n0, As, Bs);
   else
-    gemm_tile<TNT, ADDITIVE>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, qvec, score, m0, n0, As, Bs);
+    gemm_tile<TNT, ADDITIVE>(X, n_rows_x, ar, row_ids, M, K, wr, N, Y, ldy, qvec, score, m0, n0, As, Bs);
 }
 
 // ---------------------------------------------------------------------------
@@ -247,7 +247,7 @@ __device__ __forceinline__ void split4(const float4 v, bf16x4& h, bf16x4& m, bf1
 
 template <int TNW, int BMT>
 __device__ __forceinline__ void gemm_x6_tile(
-    const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
+    const float* __restrict__ X, int64_t n_rows_x, ARows ar, const int64_t* __restrict__ row_ids,
     int64_t M, int K, const WeightRows& wr, int N, float* __restrict__ Y, int64_t ldy,
     int64_t m0, int n0, __bf16* __restrict__ As, __bf16* __restrict__ Bs) {
   constexpr int BN = 32 * TNW;
@@ -268,7 +268,7 @@ __device__ __forceinline__ void gemm_x6_tile(
     a_bad[p] = false;
     if (m < M) {
       const int64_t r = row_ids ? row_ids[m] : m;
-      if ((uint64_t)r < (uint64_t)n_rows_x) a_src[p] = X + r * K;
+      if ((uint64_t)r < (uint64_t)n_rows_x) a_src[p] = X + ar.offset(r);
       else a_bad[p] = true;  // invalid id: the row becomes NaN
     }
   }
@@ -396,7 +396,7 @@ __device__ __forceinline__ void gemm_x6_tile(
 // 4 x 192 + 132) runs the 160-wide instantiation so its two wave columns
 // stay balanced (5 + 4 live N tiles instead of 6 + 3).
 __global__ __launch_bounds__(kThreads, 3) void gemm_x6_kernel(
-    const float* __restrict__ X, int64_t n_rows_x, const int64_t* __restrict__ row_ids,
+    const float* __restrict__ X, int64_t n_rows_x, ARows ar, const int64_t* __restrict__ row_ids,
     int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy, int n_col_tiles) {
   __shared__ __attribute__((aligned(16))) __bf16 As[3 * XBM * XLD];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * 192 * XLD];
@@ -405,9 +405,9 @@ __global__ __launch_bounds__(kThreads, 3) void gemm_x6_kernel(
   const int64_t m0 = (int64_t)(wg / n_col_tiles) * XBM;
   const int n0 = ct * 192;
   if (N - n0 > 160)
-    gemm_x6_tile<6, XBM>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
+    gemm_x6_tile<6, XBM>(X, n_rows_x, ar, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
   else
-    gemm_x6_tile<5, XBM>(X, n_rows_x, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
+    gemm_x6_tile<5, XBM>(X, n_rows_x, ar, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
 }
 
 constexpr int TN_STORE = 12;     // BN = 192: N = 900 -> 4 column tiles of 192 + one of 144
@@ -419,8 +419,17 @@ constexpr int TN_ADDITIVE = 13;  // BN = 208 >= Q = 200: one column tile
 int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
                           int K, const WeightRows& w, int N, float* Y, int64_t ldy,
                           hipStream_t s) {
+  return launch_gemm_store_rows(X, n_rows_x, contiguous_rows(K), row_ids, M, K, w, N, Y, ldy, s);
+}
+
+int32_t launch_gemm_store_rows(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids,
+                               int64_t M, int K, const WeightRows& w, int N, float* Y,
+                               int64_t ldy, hipStream_t s) {
   if (M == 0) return NRMS_OK;
-  if (K % 4 != 0 || ((uintptr_t)X % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  // float4 A loads: every row start must stay 16-B aligned
+  if (K % 4 != 0 || ((uintptr_t)X % 16) != 0 || ar.stride_row % 4 != 0 ||
+      (ar.per_batch != INT64_MAX && ar.stride_batch % 4 != 0))
+    return NRMS_ERR_UNSUPPORTED;
   for (int i = 0; i < w.nseg; ++i)
     if (((uintptr_t)w.w[i] % 16) != 0) return NRMS_ERR_UNSUPPORTED;
   if (gemm_arith() == NRMS_GEMM_SPLIT_BF16X6) {
@@ -431,7 +440,7 @@ int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_i
     const int64_t blocks = nrt * nct;
     if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
     hipLaunchKernelGGL(gemm_x6_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, X, n_rows_x,
-                       row_ids, M, K, w, N, Y, ldy, nct);
+                       ar, row_ids, M, K, w, N, Y, ldy, nct);
     return launch_status();
   }
   const int nct = (N + 16 * TN_STORE - 1) / (16 * TN_STORE);
@@ -443,11 +452,11 @@ int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_i
   const int rem = N % (16 * TN_STORE);
   if (rem > 0 && rem <= 16 * TN_STORE_TAIL)
     hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, TN_STORE_TAIL, false>), dim3((unsigned)blocks),
-                       dim3(kThreads), 0, s, X, n_rows_x, row_ids, M, K, w, N, Y, ldy,
+                       dim3(kThreads), 0, s, X, n_rows_x, ar, row_ids, M, K, w, N, Y, ldy,
                        (const float*)nullptr, (float*)nullptr, nct);
   else
     hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, TN_STORE, false>), dim3((unsigned)blocks),
-                       dim3(kThreads), 0, s, X, n_rows_x, row_ids, M, K, w, N, Y, ldy,
+                       dim3(kThreads), 0, s, X, n_rows_x, ar, row_ids, M, K, w, N, Y, ldy,
                        (const float*)nullptr, (float*)nullptr, nct);
   return launch_status();
 }
@@ -465,8 +474,8 @@ int32_t launch_gemm_store_f32(const float* X, int64_t M, int K, const WeightRows
   const int64_t blocks = (M + BM - 1) / BM * nct;
   if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, TN_STORE, false>), dim3((unsigned)blocks),
-                     dim3(kThreads), 0, s, X, M, (const int64_t*)nullptr, M, K, w, N, Y, ldy,
-                     (const float*)nullptr, (float*)nullptr, nct);
+                     dim3(kThreads), 0, s, X, M, contiguous_rows(K), (const int64_t*)nullptr, M, K,
+                     w, N, Y, ldy, (const float*)nullptr, (float*)nullptr, nct);
   return launch_status();
 }
 
@@ -491,8 +500,8 @@ int32_t launch_gemm_additive_score_y(const float* X, int64_t M, int K, const flo
   const int64_t blocks = (M + BM - 1) / BM;
   if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_ADDITIVE, TN_ADDITIVE, true>), dim3((unsigned)blocks),
-                     dim3(kThreads), 0, s, X, M, (const int64_t*)nullptr, M, K, w, N,
-                     y_out, (int64_t)N, q, score, 1);
+                     dim3(kThreads), 0, s, X, M, contiguous_rows(K), (const int64_t*)nullptr, M,
+                     K, w, N, y_out, (int64_t)N, q, score, 1);
   return launch_status();
 }
 

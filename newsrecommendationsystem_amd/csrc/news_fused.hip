@@ -100,8 +100,10 @@ static_assert(LDS_BYTES <= 160 * 1024, "LDS");
 // kq = lane >> 4): Wa[16 nt + n][16 c + 4 kq + t], t = 0..3 (0 past Q or D).
 // After it: a zero q|k|v row (padding titles) and a NaN row (invalid ids).
 __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __restrict__ Wa,
-                                                              float* __restrict__ WaP) {
+                                                              float* __restrict__ WaP,
+                                                              int32_t* __restrict__ recheck_count) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx == 0) *recheck_count = 0;
   if (idx >= WAP_FLOATS + SPECIAL_FLOATS) return;
   if (idx >= WAP_FLOATS) {
     const int sidx = idx - WAP_FLOATS;
@@ -120,8 +122,10 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
 // X6: WaP3[ks][nt][plane][lane][8] bf16 = plane of Wa[16 nt + (lane & 15)][32 ks + 8 (lane >> 4) + i]
 // (the B-operand fragments of v_mfma_f32_16x16x32_bf16), zero past Q or D.
 __global__ __launch_bounds__(256) void pack_additive_b3_kernel(const float* __restrict__ Wa,
-                                                               float* __restrict__ WaP) {
+                                                               float* __restrict__ WaP,
+                                                               int32_t* __restrict__ recheck_count) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx == 0) *recheck_count = 0;
   constexpr int NE = XKS * FNT * 64 * 8;
   if (idx >= NE + SPECIAL_FLOATS) return;
   if (idx >= NE) {
@@ -152,6 +156,18 @@ struct RowMap {
     const int64_t id = ids[i];
     return ((uint64_t)id < (uint64_t)n_rows) ? id : -1;
   }
+};
+
+// Rows near fp32 overflow (nrms_common.hpp, kExpRecheck). The main pass
+// (EXACT = false) takes the fast exp everywhere and appends the title groups
+// that need the reference's exp to `list` (one entry per flagging wave;
+// duplicates are harmless: the recomputation is idempotent). A second launch
+// of the same kernel (EXACT = true) walks that list with the reference's exp
+// in every row and overwrites those groups' outputs. With no such rows (all
+// real inputs), the second launch reads the zero count and exits.
+struct RecheckList {
+  int32_t* count;
+  int32_t* list;   // capacity 4 * n_groups
 };
 
 // Float offsets, within one q|k|v row, of what lane (head slot hl, x) of wave
@@ -222,11 +238,11 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 
 // MODE 0: f32 MFMA additive GEMM, fp32 context tile. MODE 1: split-bf16 x6,
 // context stored as bf16 planes.
-template <int MODE>
+template <int MODE, bool EXACT>
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const float* __restrict__ qkv, RowMap rmap, int64_t n_groups, const float* __restrict__ WaP,
-    const float* __restrict__ b_add, const float* __restrict__ q_add,
-    float* __restrict__ out NRMS_TIMING_PARAM) {
+    const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
+    RecheckList rl NRMS_TIMING_PARAM) {
   using Off = QkvOffsets;
   constexpr bool X6 = MODE == 1;
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -274,6 +290,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   // exp(d / sqrt(d_k)) as v_exp_f32(d * log2(e) / sqrt(d_k)): same overflow
   // (-> inf -> NaN) and underflow (-> 0) behaviour as the reference's exp.
   const float c_exp = 1.4426950408889634f / sqrtf((float)FDK);
+  const float sqrt_dk = sqrtf((float)FDK);
 
   // GEMM roles
   const int lm = lane & 15, kq = lane >> 4;
@@ -321,9 +338,17 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     for (int k = 0; k < FL; ++k) prefetch_v_tok(buf, k);
   };
 
-  if (blockIdx.x < n_groups) store_row(row_of(blockIdx.x), 0);
+  // iteration k of this workgroup handles title group group_at(k): k itself in
+  // the main pass, the k-th flagged group in the EXACT pass (past the end: a
+  // group of padding titles, so the prefetch of "the next group" stays valid)
+  const int64_t n_iter = EXACT ? (int64_t)*rl.count : n_groups;
+  auto group_at = [&](int64_t k) -> int64_t {
+    if constexpr (EXACT) return k < n_iter ? (int64_t)rl.list[k] : n_groups;
+    else return k;
+  };
+  if (blockIdx.x < n_iter) store_row(row_of(group_at(blockIdx.x)), 0);
   __syncthreads();
-  if (blockIdx.x < n_groups) {
+  if (blockIdx.x < n_iter) {
     prefetch_qk(0);
     prefetch_v(0);
   }
@@ -333,7 +358,8 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #endif
 
   int it = 0;
-  for (int64_t tg = blockIdx.x; tg < n_groups; tg += gridDim.x, ++it) {
+  for (int64_t k = blockIdx.x; k < n_iter; k += gridDim.x, ++it) {
+    const int64_t tg = group_at(k);
     const int nbuf = (it + 1) & 1;
     // (no barrier here: the context tile's last readers, the previous group's
     // B mainloop, finished before its B -> C barrier; C reads registers + part)
@@ -349,13 +375,14 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       // epilogue (past the last group: zero rows, so the prefetch is
       // unconditional and its registers are dead during the GEMM); stored at
       // the end of this phase
-      const int64_t next_row = row_of(tg + gridDim.x);
+      const int64_t next_row = row_of(group_at(k + gridDim.x));
       // S^T tiles: rows = keys 4j + r (A = K), cols = queries 4i + x (B = Q)
       floatx4 S[5][5];
 #pragma unroll
       for (int j = 0; j < 5; ++j)
 #pragma unroll
         for (int i = 0; i < 5; ++i) S[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      uint64_t recheck = 0;   // lanes whose row needs the reference's exp (RecheckList)
       // One query column i at a time (S^T, exp, ctx^T, split + store), so a
       // column's S registers die before the next column's are written: short
       // live ranges, no spills (all S^T first, then all ctx^T: 2 % slower;
@@ -374,10 +401,14 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         for (int j = 0; j < 5; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            const float e = __builtin_amdgcn_exp2f(S[j][i][r] * c_exp);
+            const float e = EXACT ? ref_exp(S[j][i][r], sqrt_dk)
+                                  : __builtin_amdgcn_exp2f(S[j][i][r] * c_exp);
             S[j][i][r] = e;
             sum += e;
           }
+        // rows near fp32 overflow (or non-finite): flagged (no branch here),
+        // recomputed by the EXACT pass (RecheckList)
+        if constexpr (!EXACT) recheck |= __builtin_amdgcn_ballot_w64(exp_row_needs_recheck(sum));
         const float inv = 1.0f / (sum + 1e-8f);
 #pragma unroll
         for (int j = 0; j < 5; ++j)
@@ -429,6 +460,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         s_exp(i);
         o_mfma(i);
         o_store(i);
+      }
+      if constexpr (!EXACT) {
+        if (recheck != 0 && lane == 0) rl.list[atomicAdd(rl.count, 1)] = (int32_t)tg;
       }
       store_row(next_row, nbuf);
     }
@@ -616,7 +650,12 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 
 }  // namespace
 
-size_t fused_news_packed_b_floats() { return (size_t)WAP_MAX + SPECIAL_FLOATS; }
+// packed W_add + special rows, then the recheck counter and list (int32)
+static size_t fused_news_list_offset() { return (size_t)WAP_MAX + SPECIAL_FLOATS; }
+size_t fused_news_workspace_floats(int64_t n_titles) {
+  const int64_t n_groups = (n_titles + FT - 1) / FT;
+  return fused_news_list_offset() + 4 + 4 * (size_t)n_groups;
+}
 
 bool fused_news_supported(int L, int D, int H, int Q) {
   return L == FL && D == FD && H == FH && Q == FQ;
@@ -631,29 +670,30 @@ unsigned long long* g_fused_dbg = nullptr;   // set by profiles/probes/news_vari
 
 int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
-                          const float* w_add, const float* b_add, const float* q_add, float* wap,
+                          const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s) {
   if (n_titles == 0) return NRMS_OK;
-  if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16) return NRMS_ERR_UNSUPPORTED;
+  if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
+  const int64_t n_groups = (n_titles + FT - 1) / FT;
+  if (4 * n_groups > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   const bool x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6;
-  const int mode = x6 ? 1 : 0;
-  auto kern = mode == 1 ? &fused_news_kernel<1> : &fused_news_kernel<0>;
-  const size_t lds_bytes = mode == 1 ? LDS_BYTES_X6 : LDS_BYTES;
-  static bool attr_done[2] = {false, false};
-  if (!attr_done[mode]) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes);
-    attr_done[mode] = true;
-  }
+  auto kern = x6 ? &fused_news_kernel<1, false> : &fused_news_kernel<0, false>;
+  auto kern_exact = x6 ? &fused_news_kernel<1, true> : &fused_news_kernel<0, true>;
+  const size_t lds_bytes = x6 ? LDS_BYTES_X6 : LDS_BYTES;
+  ensure_dynamic_lds(reinterpret_cast<const void*>(kern), (int)lds_bytes);
+  ensure_dynamic_lds(reinterpret_cast<const void*>(kern_exact), (int)lds_bytes);
+  int32_t* rcount = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
+  const RecheckList rl{rcount, rcount + 4};
   if (x6) {
     const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
-    hipLaunchKernelGGL(pack_additive_b3_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap);
+    hipLaunchKernelGGL(pack_additive_b3_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
+                       rcount);
   } else {
     const int npk = WAP_FLOATS + SPECIAL_FLOATS;
-    hipLaunchKernelGGL(pack_additive_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap);
+    hipLaunchKernelGGL(pack_additive_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
+                       rcount);
   }
   if (int32_t st = launch_status()) return st;
-  const int64_t n_groups = (n_titles + FT - 1) / FT;
   int dev = 0, n_cu = 256;
   if (hipGetDevice(&dev) == hipSuccess) {
     int v = 0;
@@ -662,8 +702,13 @@ int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a
   }
   const int64_t blocks = n_groups < n_cu ? n_groups : n_cu;   // persistent: one workgroup per CU
   RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows};
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, rm, n_groups,
-                     wap, b_add, q_add, out NRMS_TIMING_ARG);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, rm, n_groups, ws,
+                     b_add, q_add, out, rl NRMS_TIMING_ARG);
+  if (int32_t st = launch_status()) return st;
+  // the recheck pass: reads the count the main pass left; exits at once when 0
+  const int64_t blocks_x = blocks < 64 ? blocks : 64;
+  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes, s, qkv, rm,
+                     n_groups, ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
   return launch_status();
 }
 

@@ -35,6 +35,22 @@ __device__ __forceinline__ float4 nan4() {
 // more than 64 rows are read through L2 instead of LDS).
 constexpr int kMaxSeqLen = 4096;
 
+// Raw-exp attention weights (ScaledDotProductAttention, multihead_self.py:
+// 16-20): the reference computes e = exp(fl(d / sqrt(d_k))) in fp32 with NO max
+// subtraction, then e / (sum e + 1e-8). The kernels take a fast path, one
+// v_exp_f32 of d * log2(e) / sqrt(d_k) (a few ulp from expf), which can differ
+// from the reference only where a row comes within ulps of fp32 overflow:
+// e = inf there gives NaN weights, sum = inf gives zero weights. A row whose
+// fast sum reaches kExpRecheck (2^120: a score of at least ~80, never seen in
+// practice) or is not finite is recomputed with the reference's own arithmetic
+// (ref_exp: correctly rounded division, ~1-ulp expf), so those boundaries fall
+// where torch's do (tests/test_gpu_flow.py, overflow fixture at +-2 steps).
+constexpr float kExpRecheck = 0x1p120f;
+__device__ __forceinline__ bool exp_row_needs_recheck(float fast_sum) {
+  return !(fast_sum < kExpRecheck);
+}
+__device__ __forceinline__ float ref_exp(float d, float sqrt_dk) { return expf(d / sqrt_dk); }
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -91,12 +107,35 @@ struct WeightRows {
 // Process-wide GEMM arithmetic (nrms_set_gemm_arith; defined in capi.hip).
 int gemm_arith();
 
+// hipFuncAttributeMaxDynamicSharedMemorySize for `fn` on the calling thread's
+// current device, set once per (device, kernel, size); thread-safe (capi.hip).
+void ensure_dynamic_lds(const void* fn, int bytes);
+
+// Addressing of a GEMM's A rows: logical row r (after the optional id
+// indirection) lives at X + (r / per_batch) * stride_batch + (r % per_batch) *
+// stride_row floats. The plain contiguous case is per_batch = INT64_MAX,
+// stride_row = K; a [B, N, K] view with strides (sb, sn, 1) is per_batch = N.
+struct ARows {
+  int64_t per_batch;
+  int64_t stride_batch;
+  int64_t stride_row;
+  __host__ __device__ __forceinline__ int64_t offset(int64_t r) const {
+    return per_batch == INT64_MAX ? r * stride_row
+                                  : (r / per_batch) * stride_batch + (r % per_batch) * stride_row;
+  }
+};
+inline ARows contiguous_rows(int K) { return ARows{INT64_MAX, 0, K}; }
+
 // Host-side launchers (defined in the .hip files).
 int32_t launch_gather(const int64_t* ids, int64_t n_tok, const float* table, int64_t V, int D,
                       float* out, hipStream_t s);
 int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
                           int K, const WeightRows& w, int N, float* Y, int64_t ldy,
                           hipStream_t s);
+// Same, A rows addressed through `ar` (strided [B, N, K] input views).
+int32_t launch_gemm_store_rows(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids,
+                               int64_t M, int K, const WeightRows& w, int N, float* Y,
+                               int64_t ldy, hipStream_t s);
 int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
                                    const float* b, const float* q, int N, float* score,
                                    hipStream_t s);
@@ -129,8 +168,8 @@ int32_t launch_transpose(const float* const* src, int nseg, int seg_rows, int co
                          hipStream_t s);
 int32_t launch_embedding_backward(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
                                   int D, int64_t padding_idx, float* dtable, hipStream_t s);
-int32_t launch_adam_multi(const nrms_adam_tensor_t* ts, int n, int64_t total_blocks, float lr,
-                          float b1, float b2, float eps, int64_t step, hipStream_t s);
+int32_t launch_adam_multi(const nrms_adam_tensor_t* ts, int n, float lr, float b1, float b2,
+                          float eps, int64_t step, hipStream_t s);
 int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                     float b2, float eps, int64_t step, hipStream_t s);
 
@@ -138,11 +177,12 @@ size_t fused_user_packed_b_floats();
 bool fused_user_supported(int L, int D, int H, int Q);
 int32_t launch_fused_user(const float* qkv, int64_t B, int L, const float* w_add, const float* b_add,
                           const float* q_add, float* wap, float* out, hipStream_t s);
-size_t fused_news_packed_b_floats();
+// workspace of launch_fused_news: packed W_add, special rows, recheck list
+size_t fused_news_workspace_floats(int64_t n_titles);
 bool fused_news_supported(int L, int D, int H, int Q);
 int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
-                          const float* w_add, const float* b_add, const float* q_add, float* wap,
+                          const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s);
 int32_t launch_score_pairs(const float* news, int64_t n_news, const float* user, int64_t n_users,
                            const int64_t* news_idx, const int64_t* user_idx, int64_t n_pairs,

@@ -480,16 +480,24 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p,
   p[i] -= (lr / bc1) * (mi / denom);
 }
 
-// Multi-tensor Adam: block b belongs to the tensor whose [first_block,
-// next first_block) range holds it (n is small: a linear scan).
-__global__ __launch_bounds__(256) void adam_multi_kernel(const nrms_adam_tensor_t* __restrict__ ts,
-                                                         int n, float lr, float b1, float b2,
-                                                         float eps, float bc1, float bc2_sqrt) {
+// Multi-tensor Adam: up to kAdamChunk descriptors travel BY VALUE in the
+// kernel arguments (48 B each, 1.5 KB of the 4 KB kernarg segment), so no
+// device-side table has to outlive the launch or follow the caller's stream.
+// Block b belongs to the tensor whose [first_block, next first_block) range
+// holds it (n is small: a linear scan over SGPR-uniform data).
+constexpr int kAdamChunk = 32;
+struct AdamChunk {
+  nrms_adam_tensor_t t[kAdamChunk];
+  int64_t first_block[kAdamChunk];
+};
+__global__ __launch_bounds__(256) void adam_multi_kernel(const AdamChunk c, int n, float lr,
+                                                         float b1, float b2, float eps, float bc1,
+                                                         float bc2_sqrt) {
   const int64_t b = blockIdx.x;
   int t = 0;
-  while (t + 1 < n && ts[t + 1].first_block <= b) ++t;
-  const nrms_adam_tensor_t d = ts[t];
-  const int64_t i = (b - d.first_block) * 256 + threadIdx.x;
+  while (t + 1 < n && c.first_block[t + 1] <= b) ++t;
+  const nrms_adam_tensor_t d = c.t[t];
+  const int64_t i = (b - c.first_block[t]) * 256 + threadIdx.x;
   if (i >= d.numel) return;
   const float gi = d.grad[i];
   const float mi = d.exp_avg[i] + (1.0f - b1) * (gi - d.exp_avg[i]);
@@ -603,15 +611,26 @@ int32_t launch_embedding_backward(const int64_t* ids, int64_t n_tok, const float
   return launch_status();
 }
 
-int32_t launch_adam_multi(const nrms_adam_tensor_t* ts, int n, int64_t total_blocks, float lr,
-                          float b1, float b2, float eps, int64_t step, hipStream_t s) {
-  if (n == 0 || total_blocks == 0) return NRMS_OK;
-  if (total_blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+int32_t launch_adam_multi(const nrms_adam_tensor_t* ts, int n, float lr, float b1, float b2,
+                          float eps, int64_t step, hipStream_t s) {
   const float bc1 = (float)(1.0 - pow((double)b1, (double)step));
   const float bc2_sqrt = (float)sqrt(1.0 - pow((double)b2, (double)step));
-  hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)total_blocks), dim3(256), 0, s, ts, n, lr, b1,
-                     b2, eps, bc1, bc2_sqrt);
-  return launch_status();
+  for (int base = 0; base < n; base += kAdamChunk) {
+    AdamChunk c{};
+    const int k = n - base < kAdamChunk ? n - base : kAdamChunk;
+    int64_t blocks = 0;
+    for (int i = 0; i < k; ++i) {
+      c.t[i] = ts[base + i];
+      c.first_block[i] = blocks;
+      blocks += (ts[base + i].numel + 255) / 256;
+    }
+    if (blocks == 0) continue;
+    if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(adam_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, s, c, k, lr, b1, b2,
+                       eps, bc1, bc2_sqrt);
+    if (int32_t st = launch_status()) return st;
+  }
+  return NRMS_OK;
 }
 
 int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,

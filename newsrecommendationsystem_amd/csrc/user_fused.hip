@@ -141,7 +141,9 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     const float rs = 1.4426950408889634f / sqrtf((float)UDK);
     // Keys j >= L read row L-1 and get weight 0 (no per-key branch, so the
     // independent dot products interleave); adding 0 changes no sum.
-    auto raw = [&](int j) {
+    const float sqrt_dk = sqrtf((float)UDK);
+    bool exact = false;   // the row's weights take the reference's exp (kExpRecheck)
+    auto dot = [&](int j) {
       const int jj = j < L ? j : L - 1;
       const float4* kr = reinterpret_cast<const float4*>(tile + jj * URS + UDK * h);
       float d = 0.f;
@@ -153,8 +155,10 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         d = fmaf(q[4 * t + 2], k4.z, d);
         d = fmaf(q[4 * t + 3], k4.w, d);
       }
-      return j < L ? __builtin_amdgcn_exp2f(d * rs) : 0.f;
+      return d;
     };
+    auto raw = [&](int j) { return j < L ? __builtin_amdgcn_exp2f(dot(j) * rs) : 0.f; };
+    auto raw_exact = [&](int j) { return j < L ? ref_exp(dot(j), sqrt_dk) : 0.f; };
     // LMAX = 64 would not fit the exps in registers at 16 waves: recompute
     // them in the second pass (expf is deterministic: same weights).
     constexpr bool kKeep = LMAX <= 50;
@@ -167,6 +171,16 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       if constexpr (kKeep) e[j] = x;
       sum += x;
     }
+    if (exp_row_needs_recheck(sum)) {   // rare: rows near fp32 overflow
+      exact = true;
+      sum = 0.f;
+#pragma unroll kUnroll
+      for (int j = 0; j < LMAX; ++j) {
+        const float x = raw_exact(j);
+        if constexpr (kKeep) e[j] = x;
+        sum += x;
+      }
+    }
     const float inv = 1.0f / (sum + 1e-8f);
 #pragma unroll
     for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
@@ -174,7 +188,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     for (int j = 0; j < LMAX; ++j) {
       const int jj = j < L ? j : L - 1;
       float ej;
-      if constexpr (kKeep) ej = e[j]; else ej = raw(j);
+      if constexpr (kKeep) ej = e[j]; else ej = exact ? raw_exact(j) : raw(j);
       const float a = ej * inv;
       const float4* vr = reinterpret_cast<const float4*>(tile + jj * URS + UD + UDK * h);
 #pragma unroll
@@ -361,12 +375,7 @@ template <int MODE, int LMAX, int NT>
 int32_t launch_user_inst(const float* qkv, int64_t B, int L, const float* wap, const float* b_add,
                          const float* q_add, float* out, hipStream_t s) {
   const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64) * 4;
-  static bool attr = false;
-  if (!attr) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr = true;
-  }
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>), (int)lds);
   hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
                      L, wap, b_add, q_add, out);
   return launch_status();

@@ -189,16 +189,21 @@ class UserEncoder(nn.Module):
             dev = self.additive_attention.attention_query_vector.device
             return _train.user_encode_autograd(self, user_vector.to(dev))
         dev = self.additive_attention.attention_query_vector.device
-        x = _f32(user_vector.to(dev))
+        x = user_vector.to(dev)
         B, n_clicked, D = x.shape
+        # strided [B, N, D] views (the transpose(0, 1) of src/evaluate.py:220-224)
+        # are read in place; only an inner stride != 1 or a misaligned view is copied
+        if (x.dtype != torch.float32 or x.stride(2) != 1 or x.stride(0) % 4 or x.stride(1) % 4
+                or x.data_ptr() % 16):
+            x = _f32(x)
         out = torch.empty(B, D, dtype=torch.float32, device=dev)
         if B == 0:
             return out
         w, keep = self.weights()
         nb = N.load().nrms_user_encode_workspace_size(B, n_clicked, D)
         ws = self._ws.get(nb, dev)
-        N.call("nrms_user_encode", N.ptr(x), B, n_clicked, ctypes_byref(w), N.ptr(out), N.ptr(ws),
-               ws.numel(), N.stream_handle(dev))
+        N.call("nrms_user_encode", N.ptr(x), B, n_clicked, x.stride(0), x.stride(1),
+               ctypes_byref(w), N.ptr(out), N.ptr(ws), ws.numel(), N.stream_handle(dev))
         return out
 
 

@@ -26,7 +26,6 @@ exp_avg_sq, step), so optimizer state_dicts interchange with the reference's.
 import ctypes
 import os
 
-import numpy as np
 import torch
 
 from . import _native as N
@@ -190,68 +189,90 @@ def forward_hip(model, cand_ids, clicked_ids, seed):
     return NRMSTrain.apply(model, cand_ids, clicked_ids, p, int(seed), *model_params(model))
 
 
+class _AdamTensor(ctypes.Structure):
+    """nrms_adam_tensor_t (include/nrms_hip.h)."""
+    _fields_ = [("param", ctypes.c_void_p), ("grad", ctypes.c_void_p), ("exp_avg", ctypes.c_void_p),
+                ("exp_avg_sq", ctypes.c_void_p), ("numel", ctypes.c_int64),
+                ("first_block", ctypes.c_int64)]
+
+
 class HipAdam(torch.optim.Optimizer):
     """torch.optim.Adam (amsgrad=False, weight_decay=0, maximize=False) on the
-    HIP update kernel; same state keys. A parameter group whose parameters all
-    have gradients and the same step count is updated in ONE
-    nrms_adam_step_multi launch (a device table of per-tensor descriptors);
-    otherwise one nrms_adam_step launch per parameter."""
+    HIP update kernel; same state keys (step, exp_avg, exp_avg_sq), so
+    optimizer state_dicts interchange with the reference's
+    (src/train.py:127,233). The parameters of a group that share a step count
+    (the usual case) are updated by nrms_adam_step_multi: the descriptors go
+    to the device by value in the kernel arguments (32 per launch), so nothing
+    device-side outlives the launch or depends on the current stream.
+    Parameters whose step count differs (a parameter that had no gradient on
+    some earlier steps) are updated one nrms_adam_step launch each; so is
+    everything when NRMS_ADAM_PER_PARAM is set.
 
-    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8):
-        super().__init__(params, dict(lr=lr, betas=betas, eps=eps))
-        # per group: (descriptor rows, device table, pinned staging copy, copy event).
-        # The table is rebuilt only when a pointer changes (gradients set to None
-        # and re-allocated usually come back at the same addresses).
-        self._tables = {}
+    The update writes parameter memory through raw pointers, which torch does
+    not see; step() therefore bumps every updated parameter's version counter,
+    as an in-place torch op would, so version-keyed caches (NewsEncoder's
+    folded Q|K|V table, nrms.py) see the change."""
+
+    def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=0,
+                 amsgrad=False, *, maximize=False, foreach=None, capturable=False,
+                 differentiable=False, fused=None, decoupled_weight_decay=False):
+        # torch.optim.Adam's param_group fields, so state_dicts interchange both
+        # ways (checkpoint.py); only the reference's configuration is computed
+        super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+                                      amsgrad=amsgrad, maximize=maximize, foreach=foreach,
+                                      capturable=capturable, differentiable=differentiable,
+                                      fused=fused, decoupled_weight_decay=decoupled_weight_decay))
         self._multi = os.environ.get("NRMS_ADAM_PER_PARAM") is None
+
+    @staticmethod
+    def _check(p):
+        if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous()):
+            raise TypeError("HipAdam needs contiguous float32 CUDA parameters "
+                            f"(got {p.dtype}, device {p.device}, contiguous={p.is_contiguous()})")
 
     @torch.no_grad()
     def step(self, closure=None):
-        loss = closure() if closure is not None else None
-        for gi, group in enumerate(self.param_groups):
+        loss = None
+        if closure is not None:
+            with torch.enable_grad():
+                loss = closure()
+        updated = []
+        for group in self.param_groups:
+            if group.get("weight_decay", 0) or group.get("amsgrad") or group.get("maximize"):
+                raise NotImplementedError("HipAdam computes Adam with weight_decay=0, "
+                                          "amsgrad=False, maximize=False (src/train.py:127)")
             b1, b2 = group["betas"]
-            live = []
+            args = (ctypes.c_float(group["lr"]), ctypes.c_float(b1), ctypes.c_float(b2),
+                    ctypes.c_float(group["eps"]))
+            by_step = {}    # (device, step) -> [(p, g, state)]
             for p in group["params"]:
                 if p.grad is None:
                     continue
+                self._check(p)
+                if p.grad.is_sparse:
+                    raise RuntimeError("HipAdam does not support sparse gradients")
                 state = self.state[p]
                 if not state:
                     state["step"] = torch.tensor(0.0)
-                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
-                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    state["exp_avg"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
+                    state["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.contiguous_format)
                 state["step"] += 1
-                g = p.grad if p.grad.is_contiguous() else p.grad.contiguous()
-                live.append((p, g, state))
-            if not live:
-                continue
-            steps = {int(st["step"].item()) for _, _, st in live}
-            args = (ctypes.c_float(group["lr"]), ctypes.c_float(b1), ctypes.c_float(b2),
-                    ctypes.c_float(group["eps"]))
-            dev = live[0][0].device
-            if self._multi and len(steps) == 1 and all(p.device == dev for p, _, _ in live):
-                rows, first = [], 0
-                for p, g, st in live:
-                    n = p.numel()
-                    rows.append((p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
-                                 st["exp_avg_sq"].data_ptr(), n, first))
-                    first += (n + 255) // 256
-                rows = tuple(rows)
-                ent = self._tables.get(gi)
-                if ent is None or ent[0] != rows:
-                    if ent is not None:
-                        ent[3].synchronize()   # the old staging copy has been consumed
-                    pinned = torch.from_numpy(np.array(rows, dtype=np.int64)).pin_memory()
-                    table = torch.empty(pinned.shape, dtype=torch.int64, device=dev)
-                    table.copy_(pinned, non_blocking=True)
-                    ev = torch.cuda.Event()
-                    ev.record()
-                    ent = (rows, table, pinned, ev)
-                    self._tables[gi] = ent
-                N.call("nrms_adam_step_multi", N.ptr(ent[1]), len(live), first, *args,
-                       steps.pop(), N.stream_handle(dev))
-            else:
-                for p, g, st in live:
-                    N.call("nrms_adam_step", N.ptr(p), N.ptr(g), N.ptr(st["exp_avg"]),
-                           N.ptr(st["exp_avg_sq"]), p.numel(), *args, int(st["step"].item()),
-                           N.stream_handle(p.device))
+                g = p.grad.float().contiguous()
+                by_step.setdefault((p.device, int(state["step"].item())), []).append((p, g, state))
+            for (dev, step), live in by_step.items():
+                stream = N.stream_handle(dev)
+                if self._multi and len(live) > 1:
+                    arr = (_AdamTensor * len(live))(*[
+                        _AdamTensor(p.data_ptr(), g.data_ptr(), st["exp_avg"].data_ptr(),
+                                    st["exp_avg_sq"].data_ptr(), p.numel(), 0)
+                        for p, g, st in live])
+                    N.call("nrms_adam_step_multi", ctypes.cast(arr, ctypes.c_void_p), len(live),
+                           *args, step, stream)
+                else:
+                    for p, g, st in live:
+                        N.call("nrms_adam_step", N.ptr(p), N.ptr(g), N.ptr(st["exp_avg"]),
+                               N.ptr(st["exp_avg_sq"]), p.numel(), *args, step, stream)
+                updated += [t for p, _, st in live for t in (p, st["exp_avg"], st["exp_avg_sq"])]
+        if updated:
+            torch.autograd.graph.increment_version(updated)
         return loss

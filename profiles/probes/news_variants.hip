@@ -53,7 +53,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&wa, h_wa.size() * 4));
   CK(hipMalloc(&b, 800));
   CK(hipMalloc(&q, 800));
-  CK(hipMalloc(&wap, nrms::fused_news_packed_b_floats() * 4));
+  CK(hipMalloc(&wap, nrms::fused_news_workspace_floats(n_titles) * 4));
   CK(hipMalloc(&out0, (size_t)n_titles * 300 * 4));
   CK(hipMalloc(&out1, (size_t)n_titles * 300 * 4));
   CK(hipMalloc(&ids, h_ids.size() * 8));

@@ -9,6 +9,8 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden", "nrms_golden.npz")
+FLOW_GOLDEN = os.path.join(ROOT, "tests", "golden", "nrms_flow_golden.npz")
+FLOW_DIR = os.path.join(ROOT, "tests", "golden", "flow")
 
 
 def pytest_configure(config):
@@ -19,6 +21,16 @@ def pytest_configure(config):
 def golden():
     with np.load(GOLDEN, allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(scope="session")
+def flow():
+    """Round-2 reference fixtures (tests/golden/gen_golden_flow.py): reference
+    evaluate(), BaseDataset batches, gradients, checkpoint, exp overflow."""
+    with np.load(FLOW_GOLDEN, allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d["dir"] = FLOW_DIR
+    return d
 
 
 @pytest.fixture(scope="session")

@@ -114,6 +114,45 @@ def test_user_vectors_noncontiguous_input(golden, gold_model, device):
     assert O.normwise_rel_err(out, golden["user_out"]).max() < TOL
 
 
+def test_user_encode_strided_views_through_c_abi(golden, gold_model, device, gemm_mode):
+    """nrms_user_encode (ABI 2) reads [B, N, D] views in place: the
+    transpose(0, 1) of src/evaluate.py:220-224 (stride_b = D, stride_n = B*D)
+    and a history slice of a wider tensor. Each equals the contiguous call
+    bitwise and the golden user_out within TOL; no copy is made."""
+    from newsrecommendationsystem_amd import _native as N
+    u_in = W.normal(int(golden["seed"]), 30, (8, 50, 300), 0.3)
+    for b, n in enumerate(golden["user_len"]):
+        u_in[b, : 50 - n] = 0.0
+    B, Nn, D = u_in.shape
+    contig = torch.from_numpy(u_in).to(device)
+    tview = contig.transpose(0, 1).contiguous().transpose(0, 1)   # [B, N, D], strides (D, B*D, 1)
+    wide = torch.zeros(B, Nn + 7, D, device=device)
+    wide[:, 7:] = contig
+    sview = wide[:, 7:]                                            # strides ((N+7)*D, D, 1)
+    w, keep = gold_model.user_encoder.weights()
+    lib = N.load()
+    nb = lib.nrms_user_encode_workspace_size(B, Nn, D)
+    ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    outs = []
+    for x in (contig, tview, sview):
+        out = torch.empty(B, D, device=device)
+        N.call("nrms_user_encode", N.ptr(x), B, Nn, x.stride(0), x.stride(1), ctypes.byref(w),
+               N.ptr(out), N.ptr(ws), nb, N.stream_handle(device))
+        outs.append(out)
+    assert tview.stride() == (D, B * D, 1) and sview.stride() == ((Nn + 7) * D, D, 1)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+    assert O.normwise_rel_err(_np(outs[1]), golden["user_out"]).max() < TOL
+    # the module path hands the view over as is (bitwise the same as the C call)
+    with torch.no_grad():
+        assert torch.equal(gold_model.get_user_vector(tview), outs[1])
+    # bad strides are rejected, not misread
+    assert lib.nrms_user_encode(N.ptr(contig), B, Nn, -1, D, ctypes.byref(w), N.ptr(outs[0]),
+                                N.ptr(ws), nb, N.stream_handle(device)) == N.NRMS_ERR_INVALID_ARG
+    assert lib.nrms_user_encode(N.ptr(contig), B, Nn, Nn * D, D + 1, ctypes.byref(w),
+                                N.ptr(outs[0]), N.ptr(ws), nb,
+                                N.stream_handle(device)) == N.NRMS_ERR_UNSUPPORTED
+
+
 @pytest.mark.parametrize("mode", [0, 1, 2])
 def test_forward_golden(golden, golden_state, device, mode, gemm_mode):
     m = _module(golden_state, int(golden["V"]), device, hip_proj_mode=mode)
