@@ -7,9 +7,12 @@ mode) over a batch of B synthetic MIND-shaped impressions resident in HBM:
 1+K = 5 candidate titles and 50 clicked titles of 20 tokens each (history
 left-padded with all-zero titles, src/dataset.py:79-83), V = 70,976 words,
 d = 300, 15 heads, query dim 200 — every title is encoded (forward semantics).
-For N > 1 (torch.distributed.run, one process per GPU) each rank scores its
-own user shard of B impressions (weak scaling, no data-path collective); the
-time is the max over ranks. Rank 0 prints one JSON line.
+The impressions come from the config-4 stream (newsrecommendationsystem_amd/
+stream.py: 2,000,000 impressions over 1,000,000 users, sharded by
+user_id % world): by default each rank scores the first B impressions of its
+user shard every step (weak scaling, no data-path collective); with --stream
+the ranks score the whole stream once (config 4, strong scaling). The time
+is the max over ranks. Rank 0 prints one JSON line.
 
 Extra fields: per-stage milliseconds (HIP events on the launch stream), the
 roofline of the dominant kernel, and the CPU baseline (oracle ATen-order
@@ -37,6 +40,14 @@ def synth_titles(gen, n, V, device):
     ids = torch.randint(1, V, (n, L), generator=gen, device=device)
     lens = torch.randint(5, L + 1, (n, 1), generator=gen, device=device)
     return torch.where(torch.arange(L, device=device)[None] < lens, ids, torch.zeros_like(ids))
+
+
+def stream_impressions(rank, world, B, device, seed=0, n_impressions=None):
+    """The first B impressions of this rank's user shard of the config-4
+    stream (all of them when B is None), on the device."""
+    from newsrecommendationsystem_amd import stream as S
+    idx = S.shard(seed, rank, world, n_impressions or S.N_IMPRESSIONS, S.N_USERS, device)
+    return idx if B is None else idx[:B]
 
 
 def synth_impressions(seed, B, V, device):
@@ -72,29 +83,51 @@ def load_traffic(kernel):
         return None
 
 
-def cpu_baseline(model, device, sample_B=32, min_seconds=12.0, max_reps=500):
-    """Time the oracle's ATen-order CPU restatement (oracle/nrms_torch_cpu.py)
-    on a bounded sample of the same workload; also check GPU parity on it."""
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(model, cand, clk, reps=3):
+    """SURVEY §8d CPU leg: the oracle's ATen-order restatement of the
+    reference forward (oracle/nrms_torch_cpu.py, bit-exact with the reference
+    on the golden vectors) on the SAME batch as the GPU step (B impressions),
+    median of `reps` timed runs after one warm-up, on this process's CPU
+    share (OMP_NUM_THREADS / affinity); also the GPU-vs-CPU logits parity on
+    that batch."""
     from oracle import nrms_torch_cpu as T
-    cand, clk = synth_impressions(424242, sample_B, V_WORDS, device)
+    threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
     sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     cand_c, clk_c = cand.cpu(), clk.cpu()
-    threads = torch.get_num_threads()
-    with torch.no_grad():
-        ref = T.forward(cand_c, clk_c, sd)  # warm
-        reps, t0 = 0, time.perf_counter()
-        while reps < max_reps and (reps == 0 or time.perf_counter() - t0 < min_seconds):
-            ref = T.forward(cand_c, clk_c, sd)
-            reps += 1
-        dt = time.perf_counter() - t0
-        gpu = model.forward_ids(cand, clk).cpu()
+    times = []
+    try:
+        with torch.no_grad():
+            ref = T.forward(cand_c, clk_c, sd)   # warm
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                ref = T.forward(cand_c, clk_c, sd)
+                times.append(time.perf_counter() - t0)
+            gpu = model.forward_ids(cand, clk).cpu()
+    finally:
+        torch.set_num_threads(prev)
+    B = cand.shape[0]
+    med = sorted(times)[len(times) // 2]
     err = float(((gpu - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-30)).max())
-    value = sample_B * reps / dt
-    info = {"value": round(value, 2), "unit": "impressions/s", "cores": threads, "kind": "port",
-            "sample": f"{reps} x NRMS.forward over {sample_B} impressions (1+K=5, 50 clicked, L=20, "
+    info = {"value": round(B / med, 2), "unit": "impressions/s", "cores": threads, "kind": "port",
+            "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "sample": f"NRMS.forward over the bench batch ({B} impressions, 1+K=5, 50 clicked, L=20, "
                       f"V={V_WORDS}) via oracle/nrms_torch_cpu.py, torch {torch.__version__}, "
-                      f"{threads} threads, {dt:.1f} s"}
-    parity = {"sample_impressions": sample_B, "max_normwise_rel_err_logits": err,
+                      f"{threads} threads, median of {reps} runs "
+                      f"({', '.join(f'{t:.2f}' for t in times)} s)"}
+    parity = {"sample_impressions": B, "max_normwise_rel_err_logits": err,
               "tolerance": 1e-3, "ok": bool(err <= 1e-3)}
     return info, parity
 
@@ -193,16 +226,54 @@ def news_encoder_cfg2(model, device, n_titles=100_000, reps=10):
             "titles_per_s": round(n_titles / (ms / 1e3), 1)}
 
 
+PEAK_TFLOPS_BF16 = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
+
+
+def load_sq(kernel):
+    """MFMA-busy fraction and VALU:MFMA ratio of `kernel` from the committed
+    SQ counter passes (profiles/sq_counters.json, made by profiles/sq_summary.py
+    from rocprofv3 --pmc runs), or None."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "sq_counters.json")) as f:
+            return json.load(f).get(kernel)
+    except (OSError, ValueError):
+        return None
+
+
+def issue_floor_ms(stage, w, gemm):
+    """Time the dominant stage's matrix / vector instructions need at the
+    MI355X peaks with nothing else in the way (SURVEY §8d FLOP split): the
+    x6 GEMM issues 6 bf16 products per fp32 product (2.5 PF dense), exact f32
+    MFMA and the attention contractions run at 157.3 TF, pooling on VALU."""
+    if stage != "news_fused":
+        return None
+    f = w["split"]
+    gemm_s = f["gemm"] * 6 / (PEAK_TFLOPS_BF16 * 1e12) if gemm == "x6" else f["gemm"] / (PEAK_TFLOPS_F32 * 1e12)
+    rest_s = (f["attention"] + f["pool"]) / (PEAK_TFLOPS_F32 * 1e12)
+    return (gemm_s + rest_s) * 1e3
+
+
+def run_plan_steps(plan, batches, steps, events=None):
+    for k in range(steps):
+        cand, clk = batches[k % len(batches)]
+        plan.run(cand, clk, events[k] if events else None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=None,
+                    help="timed steps (default 50; with --stream: every batch of the shard)")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=1024, help="impressions per GPU per step")
     ap.add_argument("--proj", choices=["folded", "direct", "auto"], default="folded")
+    ap.add_argument("--stream", action="store_true",
+                    help="BASELINE cfg4: score the whole user-sharded 2M-impression stream once "
+                         "(strong scaling; --steps is then the number of batches, 0 = all)")
+    ap.add_argument("--stream-impressions", type=int, default=None)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="separate MHSA / additive / pool kernels")
-    ap.add_argument("--no-extras", action="store_true", help="skip the gather / config-2 figures")
+    ap.add_argument("--no-extras", action="store_true", help="skip the gather / config-2 / direct figures")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend for the barrier / max-over-ranks timing (nccl = RCCL); "
                          "gloo lets several ranks share one GPU for a rehearsal")
@@ -226,32 +297,49 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     from newsrecommendationsystem_amd import _native as Nat
+    from newsrecommendationsystem_amd import stream as S
     from newsrecommendationsystem_amd.pipeline import ForwardPlan
 
     Nat.load().nrms_set_gemm_arith(Nat.NRMS_GEMM_SPLIT_BF16X6 if args.gemm == "x6" else Nat.NRMS_GEMM_F32)
     mode = {"folded": Nat.NRMS_PROJ_FOLDED, "direct": Nat.NRMS_PROJ_DIRECT, "auto": Nat.NRMS_PROJ_AUTO}[args.proj]
     model = build_model(device)
     B = args.batch
-    cand, clk = synth_impressions(1000 + rank, B, V_WORDS, device)   # this rank's user shard
+    # this rank's user shard of the config-4 stream (user_id % world); inputs
+    # are generated into HBM before the timed region
+    idx = stream_impressions(rank, world, None if args.stream else B, device,
+                             n_impressions=args.stream_impressions)
+    if args.stream:
+        batches = [S.batch(0, idx[a:a + B], V_WORDS) for a in range(0, idx.numel(), B)]
+    else:
+        batches = [S.batch(0, idx, V_WORDS)]
+    full = [b for b in batches if b[0].shape[0] == B]
+    tail = [b for b in batches if b[0].shape[0] != B]
     plan = ForwardPlan(model, B, C, N_CLICKED, L, proj_mode=mode, fused=not args.unfused)
+    tail_plan = (ForwardPlan(model, tail[0][0].shape[0], C, N_CLICKED, L, proj_mode=mode,
+                             fused=not args.unfused) if tail else None)
     n_st = len(plan.stages)
+    steps = 50 if args.steps is None else args.steps
+    if args.stream:
+        steps = len(full) if not args.steps or args.steps > len(full) else args.steps
+    cand, clk = full[0]
 
     with torch.no_grad():
-        for _ in range(args.warmup):
-            plan.run(cand, clk)
+        run_plan_steps(plan, full, args.warmup)
+        if tail_plan is not None:
+            tail_plan.run(*tail[0])
         # one un-timed check that the plan equals the fused C-ABI forward
         y_plan = plan.run(cand, clk).clone()
         y_fwd = model.forward_ids(cand, clk, proj_mode=mode)
         same = bool(torch.equal(y_plan, y_fwd))
-        events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_st + 1)]
-                  for _ in range(args.steps)]
+        events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_st + 1)] for _ in range(steps)]
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for k in range(args.steps):
-            plan.run(cand, clk, events[k])
+        run_plan_steps(plan, full, steps, events)
+        if args.stream and tail_plan is not None and steps == len(full):
+            tail_plan.run(*tail[0])
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -264,11 +352,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    stage_ms = {s: 0.0 for s in plan.stages}
+    stage_ms = {st: 0.0 for st in plan.stages}
     for ev in events:
-        for i, s in enumerate(plan.stages):
-            stage_ms[s] += ev[i].elapsed_time(ev[i + 1])
-    stage_ms = {s: v / args.steps for s, v in stage_ms.items()}
+        for i, st in enumerate(plan.stages):
+            stage_ms[st] += ev[i].elapsed_time(ev[i + 1])
+    stage_ms = {st: v / steps for st, v in stage_ms.items()}
     work = plan.work()
     dom = max(stage_ms, key=stage_ms.get)
     w = work[dom]
@@ -279,32 +367,73 @@ def main():
     else:
         achieved, peak, unit, bound = w["bytes"] / t_dom / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
 
-    ms_per_step = elapsed / args.steps * 1e3
-    value = world * B * args.steps / elapsed
+    ms_per_step = elapsed / steps * 1e3
+    if args.stream:
+        done = (steps * B + (tail[0][0].shape[0] if tail and steps == len(full) else 0))
+        if dist:
+            tt = torch.tensor([float(done)], dtype=torch.float64, device=device)
+            if args.dist_backend != "nccl":
+                tt = tt.cpu()
+            dist.all_reduce(tt)
+            done = float(tt.item())
+        value = done / elapsed
+    else:
+        value = world * B * steps / elapsed
+    floor = issue_floor_ms(dom, w, args.gemm)
+    sq = load_sq(dom)
+    roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+                "frac": round(achieved / peak, 4), "traffic": load_traffic(dom),
+                "algorithmic_per_launch": {"flop": w["flop"], "bytes": w["bytes"]},
+                "peak_note": "fp32 MFMA/vector peak; the x6 GEMM issues 6 bf16 products per fp32 "
+                             "product, so see issue_floor for the instruction-level ceiling"}
+    if floor is not None:
+        roofline["issue_floor"] = {
+            "ms": round(floor, 4), "frac": round(floor / stage_ms[dom], 4),
+            "basis": ("additive GEMM x6 bf16 products at 2.5 PF dense + attention contractions "
+                      "and pooling at 157.3 TF" if args.gemm == "x6" else "all at 157.3 TF (f32 MFMA)"),
+            "flop_split": w["split"]}
+    if sq is not None:
+        roofline["sq_counters"] = sq
+    workload = ("BASELINE cfg4: full NRMS forward over the whole user-sharded stream "
+                f"({idx.numel() if not dist else 'per-rank shards of'} impressions"
+                f"{'' if dist else ' on this GPU'}), every title encoded"
+                if args.stream else
+                "BASELINE cfg3: full NRMS forward scoring (news+user encoder+click predictor), "
+                "every title encoded; batch = first B impressions of this rank's cfg4 user shard")
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "impressions/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "steps": steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "strong" if args.stream else "weak", "vs_baseline": None,
         "dtype": "fp32" if args.gemm == "f32" else "fp32 (GEMMs: exact 3-way bf16 split, 6 products, fp32 accumulate)",
-        "data": "synthetic (MIND-shaped ids, random-init weights, N(0,1) embedding table)",
-        "config": {"workload": "BASELINE cfg3: full NRMS forward scoring (news+user encoder+"
-                               "click predictor), every title encoded", "global_batch": B * world,
+        "data": "synthetic (MIND-shaped stream: counter-hash ids, random-init weights, N(0,1) embedding table)",
+        "config": {"workload": workload, "global_batch": B * world,
                    "impressions_per_gpu": B, "candidates": C, "clicked": N_CLICKED,
                    "title_len": L, "vocab": V_WORDS, "d_model": D, "heads": 15,
-                   "query_dim": 200, "proj_mode": args.proj, "gemm_arith": args.gemm, "news_tail": "unfused" if args.unfused else "fused",
+                   "query_dim": 200, "proj_mode": args.proj, "gemm_arith": args.gemm,
+                   "news_tail": "unfused" if args.unfused else "fused",
+                   "stream": {"impressions": args.stream_impressions or S.N_IMPRESSIONS,
+                              "users": S.N_USERS, "sharding": "user_id % world"},
                    "parallelism": f"user-shard x{world}"},
-        "roofline": {"kernel": dom, "bound": bound, "achieved": round(achieved, 3),
-                     "peak": peak, "unit": unit, "frac": round(achieved / peak, 4),
-                     "traffic": load_traffic(dom),
-                     "algorithmic_per_launch": {"flop": w["flop"], "bytes": w["bytes"]}},
-        "stages_ms": {s: round(v, 4) for s, v in stage_ms.items()},
+        "roofline": roofline,
+        "stages_ms": {st: round(v, 4) for st, v in stage_ms.items()},
         "plan_equals_nrms_forward": same,
     }
-    if rank == 0 and world == 1 and not args.no_extras:
+    if rank == 0 and world == 1 and not args.no_extras and not args.stream:
         out["gather_roofline"] = gather_hbm(device)
         out["news_encoder_cfg2"] = news_encoder_cfg2(model, device)
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cb, parity = cpu_baseline(model, device)
+        if args.proj == "folded":
+            dplan = ForwardPlan(model, B, C, N_CLICKED, L, proj_mode=Nat.NRMS_PROJ_DIRECT,
+                                fused=not args.unfused)
+            with torch.no_grad():
+                dplan.run(cand, clk)
+                dms = _time_launches(lambda: dplan.run(cand, clk), 10, device)
+            out["direct_projection"] = {
+                "ms_per_step": round(dms, 4), "impressions_per_s": round(B / (dms / 1e3), 1),
+                "note": "per-token Q|K|V projection (no vocabulary folding): the work SURVEY §8d's "
+                        "789.6 MFLOP/impression unit describes"}
+            del dplan
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stream:
+        cb, parity = cpu_baseline(model, cand, clk)
         out["cpu_baseline"] = cb
         out["parity_vs_cpu"] = parity
         out["auc_vs_cpu"] = eval_auc_check(model, device)

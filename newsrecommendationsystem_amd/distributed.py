@@ -8,13 +8,24 @@ The reference has no distributed code (SURVEY §0 finding 1); this module is
 new, and tests/test_distributed_cpu.py covers it with world_size 2 on gloo.
 """
 import os
+import re
 import zlib
 
 import torch
 
 
+_DIGITS = re.compile(r"^[A-Za-z_]*(\d+)$")
+
+
 def user_rank(user, world):
-    """Stable owner rank of a user id (Python's hash() is salted per process)."""
+    """Owner rank of a user: user_id % world for integer
+    ids and for MIND-style ids such as "U13740" (the number after the prefix);
+    any other string by a stable hash (Python's hash() is salted per process)."""
+    if isinstance(user, int):
+        return user % world
+    m = _DIGITS.match(str(user))
+    if m:
+        return int(m.group(1)) % world
     return zlib.crc32(str(user).encode()) % world
 
 
@@ -23,6 +34,19 @@ def shard_impressions(impressions, rank, world):
     if world <= 1:
         return list(impressions)
     return [im for im in impressions if user_rank(im.user, world) == rank]
+
+
+def all_reduce_(t, group=None):
+    """In-place SUM all-reduce of a tensor; a CUDA tensor under gloo (ranks
+    sharing one GPU in tests) goes through host memory."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(group) == "gloo":
+        host = t.cpu()
+        dist.all_reduce(host, group=group)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t, group=group)
+    return t
 
 
 def shard_rows(n, rank, world):

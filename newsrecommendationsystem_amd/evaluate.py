@@ -139,7 +139,7 @@ def evaluate(model, directory, num_workers=4, max_count=sys.maxsize, process_gro
     `directory` (news_parsed.tsv + behaviors.tsv). `num_workers` is accepted
     for compatibility (there is no process pool). With a torch.distributed
     `process_group`, each rank scores the impressions of its users
-    (zlib.crc32(user) % world) and the metric sums are all-reduced."""
+    (distributed.user_rank: user_id % world) and the metric sums are all-reduced."""
     import os
     corpus = read_news_parsed(os.path.join(directory, "news_parsed.tsv"))
     imps = read_behaviors(os.path.join(directory, "behaviors.tsv"))

@@ -137,11 +137,13 @@ class ForwardPlan:
                               bytes=n_all * L * (4 * 3 * D + (8 if self.folded else 0) + 4 * D)),
             "addscore_news": dict(flop=2 * n_all * L * D * Q, bytes=4 * (n_all * L * (D + 1) + Q * D)),
             "pool_news": dict(flop=2 * n_all * L * D, bytes=4 * (n_all * L * (D + 1) + n_all * D)),
-            # fused tail: gathered q|k|v rows + ids in, context scratch written once
-            # (re-read from L2 for pooling), news vectors out
+            # fused tail: gathered q|k|v rows + ids in, news vectors out, W_add
+            # (the context tile stays in LDS)
             "news_fused": dict(flop=att_flop(n_all, L) + 2 * n_all * L * D * Q + 2 * n_all * L * D,
-                               bytes=n_all * L * (4 * 3 * D + (8 if self.folded else 0) + 4 * D)
-                               + 4 * (n_all * D + Q * D)),
+                               bytes=n_all * L * (4 * 3 * D + (8 if self.folded else 0))
+                               + 4 * (n_all * D + Q * D),
+                               split=dict(attention=att_flop(n_all, L), gemm=2 * n_all * L * D * Q,
+                                          pool=2 * n_all * L * D)),
             "qkv_user": dict(flop=2 * n_clk * D * 3 * D, bytes=4 * (n_clk * 4 * D + 3 * D * D)),
             "mhsa_user": dict(flop=att_flop(B, Nc), bytes=4 * n_clk * 4 * D),
             "addscore_user": dict(flop=2 * n_clk * D * Q, bytes=4 * (n_clk * (D + 1) + Q * D)),

@@ -122,7 +122,8 @@ class FedAvg:
             k = p.numel()
             self.flat[off:off + k].copy_(p.detach().reshape(-1))
             off += k
-        self.dist.all_reduce(self.flat, group=self.group)
+        from .distributed import all_reduce_
+        all_reduce_(self.flat, self.group)
         self.flat.div_(self.world)
         off = 0
         for p in self.params:

@@ -476,3 +476,29 @@ def test_user_tail_beyond_fused_range(device, n_clk):
     with torch.no_grad():
         u = _np(m.get_user_vector(torch.from_numpy(vec).to(device)))
     assert O.normwise_rel_err(u, O.user_encode(vec, sd, np.float64)).max() < 1e-5
+
+
+def test_config2_news_encoder_100k_titles(device, gemm_mode):
+    """BASELINE config 2 at full size (100,000 titles x 20 tokens, V = 70,976,
+    N(0,1) table): folded == direct within fp32 rounding (normwise 1e-5),
+    encoding in two halves == one call bitwise, and a 512-title sample
+    against the fp64 oracle (normwise 1e-3 per vector)."""
+    from newsrecommendationsystem_amd import _native as N
+    V, n = 70976, 100_000
+    sd = W.nrms_state(8, V)
+    m = _module(sd, V, device, hip_cache_folded_table=False)
+    titles = torch.from_numpy(W.titles(8, 500, n, V))
+    with torch.no_grad():
+        m.config.hip_proj_mode = N.NRMS_PROJ_FOLDED
+        folded = m.get_news_vector({"title": titles})
+        halves = torch.cat([m.get_news_vector({"title": titles[:n // 2]}),
+                            m.get_news_vector({"title": titles[n // 2:]})])
+        m.config.hip_proj_mode = N.NRMS_PROJ_DIRECT
+        direct = m.get_news_vector({"title": titles})
+    assert torch.isfinite(folded).all()
+    assert torch.equal(folded, halves)
+    rel = ((folded - direct).norm(dim=1) / direct.norm(dim=1)).max()
+    assert rel < 1e-5, float(rel)
+    pick = np.sort(W.randint(8, 501, (512,), 0, n))
+    ref = O.news_encode(titles.numpy()[pick], sd, np.float64)
+    assert O.normwise_rel_err(_np(folded)[pick], ref).max() < 1e-3
