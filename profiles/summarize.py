@@ -39,8 +39,8 @@ def stage_of(name, grid_threads, wg):
         return "score"
     if "fused_user" in name:
         return "user_fused"
-    if "fused_news" in name:
-        return "news_fused"
+    if "fused_news" in name:   # the EXACT recheck launch (true) is its own line
+        return "news_recheck" if ", true>" in name else "news_fused"
     if "gather_rows_kernel" in name:
         return "gather"
     return None
