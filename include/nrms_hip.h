@@ -42,7 +42,8 @@ extern "C" {
 #endif
 
 /* 2: nrms_user_encode takes batch / row strides; nrms_adam_step_multi takes a
- *    host descriptor array (no device table, no total_blocks). */
+ *    host descriptor array (no device table, no total_blocks); q|k|v buffers
+ *    carry a row stride (nrms_qkv_row_stride). */
 #define NRMS_ABI_VERSION 2
 
 typedef enum {
@@ -100,15 +101,23 @@ int32_t nrms_last_hip_error(void);
 int32_t nrms_embedding_gather(const int64_t* ids, int64_t n_tok, const float* table,
                               int64_t V, int32_t D, float* out, hipStream_t stream);
 
-/* Q|K|V projection (multihead_self.py:53-58): qkv[m, 0:3D] = x[row(m)] [W_Q;W_K;W_V]^T
- * + [b_Q;b_K;b_V], row(m) = row_ids ? row_ids[m] : m (row_ids index x's rows,
- * n_rows_x bounds them). fp32 MFMA GEMM. */
+/* Row stride (floats) of the q|k|v rows the fused kernels prefer: 3D rounded
+ * up to whole 128-B lines (928 for D = 300). Rows at this stride are written
+ * by the projection GEMM without partial cache lines (3,600-B rows wrote
+ * 1.27x their bytes); any stride >= 3D that is a multiple of 4 is accepted. */
+int32_t nrms_qkv_row_stride(int32_t D);
+
+/* Q|K|V projection (multihead_self.py:53-58): qkv[m * ld_qkv + 0:3D] =
+ * x[row(m)] [W_Q;W_K;W_V]^T + [b_Q;b_K;b_V], row(m) = row_ids ? row_ids[m] : m
+ * (row_ids index x's rows, n_rows_x bounds them); ld_qkv = 0 means 3D.
+ * MFMA GEMM (arithmetic: nrms_set_gemm_arith). */
 int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
-                         const nrms_encoder_weights_t* w, float* qkv, hipStream_t stream);
+                         const nrms_encoder_weights_t* w, float* qkv, int64_t ld_qkv,
+                         hipStream_t stream);
 
 /* Multi-head raw-exp self-attention over sequences of length L
  * (ScaledDotProductAttention, multihead_self.py:15-23, heads concatenated
- * :74-75): for sequence s, token i reads qkv row r(s,i) = tok_ids ?
+ * :74-75) over packed q|k|v rows (stride 3D): for sequence s, token i reads qkv row r(s,i) = tok_ids ?
  * tok_ids[s*L+i] : s*L+i (tok_ids index qkv's n_rows_qkv rows). Sequences
  * s >= n_seq_a take their ids from tok_ids_b + (s-n_seq_a)*L (NULL: same
  * array). ctx[s*L+i, :] is the [D] context row. L <= 4096 (beyond 64 the
@@ -143,10 +152,11 @@ int32_t nrms_additive_pool(const float* x, const float* scores, int64_t n_seq, i
  * H = 15, Q = 200); other shapes return NRMS_ERR_UNSUPPORTED (use the stage
  * entry points). Used by nrms_news_encode* and nrms_forward when it applies. */
 size_t nrms_news_attention_pool_workspace_size(int64_t n_titles, int32_t L, int32_t D);
-int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
-                                 int64_t n_seq_a, const int64_t* tok_ids_b, int64_t n_titles,
-                                 int32_t L, const nrms_encoder_weights_t* w, float* out,
-                                 void* workspace, size_t workspace_bytes, hipStream_t stream);
+int32_t nrms_news_attention_pool(const float* qkv, int64_t ld_qkv, int64_t n_rows_qkv,
+                                 const int64_t* tok_ids, int64_t n_seq_a, const int64_t* tok_ids_b,
+                                 int64_t n_titles, int32_t L, const nrms_encoder_weights_t* w,
+                                 float* out, void* workspace, size_t workspace_bytes,
+                                 hipStream_t stream);
 
 /* NewsEncoder.forward (src/model/NRMS/news_encoder.py:27-48), eval mode:
  * ids[n_titles, L] -> out[n_titles, D]. */
@@ -157,12 +167,12 @@ int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const 
                          float* out, void* workspace, size_t workspace_bytes,
                          hipStream_t stream);
 
-/* Same, from a caller-held folded table qkv_table[V, 3D] (nrms_qkv_project of
- * the whole embedding table): lets an eval loop reuse one projection across
- * calls while the weights are unchanged. */
+/* Same, from a caller-held folded table qkv_table[V] (rows at stride ld_qkv,
+ * nrms_qkv_project of the whole embedding table; 0 = 3D): lets an eval loop
+ * reuse one projection across calls while the weights are unchanged. */
 size_t nrms_news_encode_folded_workspace_size(int64_t n_titles, int32_t L, int32_t D);
 int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
-                                const float* qkv_table, int64_t V,
+                                const float* qkv_table, int64_t ld_qkv, int64_t V,
                                 const nrms_encoder_weights_t* w, float* out,
                                 void* workspace, size_t workspace_bytes, hipStream_t stream);
 
@@ -179,12 +189,12 @@ int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N, int64_t str
                          void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Fused UserEncoder tail (user_encoder.py:15-26 after the projection): raw-exp
- * MHSA over qkv[B*N, 3D] (row b*N + i) + additive attention + pooling, one
+ * MHSA over qkv rows b*N + i (stride ld_qkv, 0 = 3D) + additive attention + pooling, one
  * workgroup per user, the context kept in LDS; out[B, D]. N <= 64, reference
  * geometry (D = 300, H = 15, Q = 200). Used by nrms_user_encode and
  * nrms_forward when it applies. Workspace: a packed copy of W_add. */
 size_t nrms_user_attention_pool_workspace_size(int64_t B, int32_t N, int32_t D);
-int32_t nrms_user_attention_pool(const float* qkv, int64_t B, int32_t N,
+int32_t nrms_user_attention_pool(const float* qkv, int64_t ld_qkv, int64_t B, int32_t N,
                                  const nrms_encoder_weights_t* w, float* out, void* workspace,
                                  size_t workspace_bytes, hipStream_t stream);
 

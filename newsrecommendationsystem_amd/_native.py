@@ -42,19 +42,21 @@ SIGNATURES = {
     "nrms_status_string": (ctypes.c_char_p, [_i32]),
     "nrms_last_hip_error": (_i32, []),
     "nrms_embedding_gather": (_i32, [_p, _i64, _p, _i64, _i32, _p, _p]),
-    "nrms_qkv_project": (_i32, [_p, _i64, _p, _i64, _EW, _p, _p]),
+    "nrms_qkv_row_stride": (_i32, [_i32]),
+    "nrms_qkv_project": (_i32, [_p, _i64, _p, _i64, _EW, _p, _i64, _p]),
     "nrms_self_attention": (_i32, [_p, _i64, _p, _i64, _p, _i64, _i32, _EW, _p, _p]),
     "nrms_additive_attention": (_i32, [_p, _i64, _i32, _EW, _p, _p, _p]),
     "nrms_additive_scores": (_i32, [_p, _i64, _EW, _p, _p]),
     "nrms_additive_pool": (_i32, [_p, _p, _i64, _i32, _i32, _p, _p]),
     "nrms_news_attention_pool_workspace_size": (_sz, [_i64, _i32, _i32]),
-    "nrms_news_attention_pool": (_i32, [_p, _i64, _p, _i64, _p, _i64, _i32, _EW, _p, _p, _sz, _p]),
+    "nrms_news_attention_pool": (_i32, [_p, _i64, _i64, _p, _i64, _p, _i64, _i32, _EW, _p, _p, _sz,
+                                         _p]),
     "nrms_news_encode_workspace_size": (_sz, [_i64, _i32, _i64, _i32, _i32]),
     "nrms_news_encode": (_i32, [_p, _i64, _i32, _p, _i64, _EW, _i32, _p, _p, _sz, _p]),
     "nrms_news_encode_folded_workspace_size": (_sz, [_i64, _i32, _i32]),
-    "nrms_news_encode_folded": (_i32, [_p, _i64, _i32, _p, _i64, _EW, _p, _p, _sz, _p]),
+    "nrms_news_encode_folded": (_i32, [_p, _i64, _i32, _p, _i64, _i64, _EW, _p, _p, _sz, _p]),
     "nrms_user_attention_pool_workspace_size": (_sz, [_i64, _i32, _i32]),
-    "nrms_user_attention_pool": (_i32, [_p, _i64, _i32, _EW, _p, _p, _sz, _p]),
+    "nrms_user_attention_pool": (_i32, [_p, _i64, _i64, _i32, _EW, _p, _p, _sz, _p]),
     "nrms_user_encode_workspace_size": (_sz, [_i64, _i32, _i32]),
     "nrms_user_encode": (_i32, [_p, _i64, _i32, _i64, _i64, _EW, _p, _p, _sz, _p]),
     "nrms_score": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p]),

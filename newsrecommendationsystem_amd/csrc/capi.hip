@@ -78,6 +78,17 @@ WeightRows qkv_rows(const nrms_encoder_weights_t* w) {
   return r;
 }
 
+// q|k|v row stride of the hot path: padded to whole 128-B lines when the fused
+// kernels take the shape, 3D (the stage kernels' layout) otherwise
+int64_t news_ld(const nrms_encoder_weights_t* w, int32_t L) {
+  return fused_news_supported(L, w->d_model, w->n_heads, w->query_dim) ? qkv_row_stride(w->d_model)
+                                                                         : 3 * (int64_t)w->d_model;
+}
+int64_t user_ld(const nrms_encoder_weights_t* w, int32_t N) {
+  return fused_user_supported(N, w->d_model, w->n_heads, w->query_dim) ? qkv_row_stride(w->d_model)
+                                                                        : 3 * (int64_t)w->d_model;
+}
+
 bool use_folded(int32_t mode, int64_t n_tok, int64_t V) {
   if (mode == NRMS_PROJ_FOLDED) return true;
   if (mode == NRMS_PROJ_DIRECT) return false;
@@ -90,7 +101,7 @@ struct NewsSizes {
 };
 NewsSizes news_sizes(int64_t n_titles, int32_t L, int64_t V, int32_t D, bool folded) {
   const size_t ntok = (size_t)n_titles * (size_t)L;
-  return {(folded ? (size_t)V : ntok) * 3 * (size_t)D, ntok * (size_t)D, ntok,
+  return {(folded ? (size_t)V : ntok) * (size_t)qkv_row_stride(D), ntok * (size_t)D, ntok,
           fused_news_workspace_floats(n_titles)};
 }
 size_t news_bytes(const NewsSizes& z) {
@@ -99,14 +110,15 @@ size_t news_bytes(const NewsSizes& z) {
 
 // attention + additive pooling from projected rows (shared by news and user
 // paths). `wap` non-null: use the fused news kernel when the geometry allows.
-int32_t encode_from_qkv(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
-                        const int64_t* ids_b, int64_t n_seq, int32_t L,
+int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
+                        int64_t n_seq_a, const int64_t* ids_b, int64_t n_seq, int32_t L,
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
                         hipStream_t s, float* wap = nullptr) {
   const int D = w->d_model;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
-    return launch_fused_news(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
+    return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
                              w->q_add, wap, out, s);
+  if (ldq != 3 * (int64_t)D) return NRMS_ERR_UNSUPPORTED;   // stage kernels: packed rows
   int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
   st = launch_gemm_additive_score(ctx, n_seq * L, D, w->w_add, w->b_add, w->q_add, w->query_dim,
@@ -151,13 +163,18 @@ int32_t nrms_embedding_gather(const int64_t* ids, int64_t n_tok, const float* ta
   return launch_gather(ids, n_tok, table, V, D, out, stream);
 }
 
+int32_t nrms_qkv_row_stride(int32_t D) { return D > 0 ? (int32_t)qkv_row_stride(D) : 0; }
+
 int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
-                         const nrms_encoder_weights_t* w, float* qkv, hipStream_t stream) {
+                         const nrms_encoder_weights_t* w, float* qkv, int64_t ld_qkv,
+                         hipStream_t stream) {
   if (M < 0 || n_rows_x < 0) return NRMS_ERR_INVALID_ARG;
   if (int32_t st = shape_ok(w)) return st;
   if (M > 0 && (!x || !qkv)) return NRMS_ERR_INVALID_ARG;
   const int D = w->d_model;
-  return launch_gemm_store(x, n_rows_x, row_ids, M, D, qkv_rows(w), 3 * D, qkv, 3 * D, stream);
+  if (ld_qkv == 0) ld_qkv = 3 * D;
+  if (ld_qkv < 3 * D) return NRMS_ERR_INVALID_ARG;
+  return launch_gemm_store(x, n_rows_x, row_ids, M, D, qkv_rows(w), 3 * D, qkv, ld_qkv, stream);
 }
 
 int32_t nrms_self_attention(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
@@ -204,10 +221,11 @@ size_t nrms_news_attention_pool_workspace_size(int64_t n_titles, int32_t L, int3
   return align_up(fused_news_workspace_floats(n_titles) * 4);   // the context stays on chip
 }
 
-int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
-                                 int64_t n_seq_a, const int64_t* tok_ids_b, int64_t n_titles,
-                                 int32_t L, const nrms_encoder_weights_t* w, float* out,
-                                 void* workspace, size_t workspace_bytes, hipStream_t stream) {
+int32_t nrms_news_attention_pool(const float* qkv, int64_t ld_qkv, int64_t n_rows_qkv,
+                                 const int64_t* tok_ids, int64_t n_seq_a, const int64_t* tok_ids_b,
+                                 int64_t n_titles, int32_t L, const nrms_encoder_weights_t* w,
+                                 float* out, void* workspace, size_t workspace_bytes,
+                                 hipStream_t stream) {
   if (n_titles < 0 || n_seq_a < 0 || L <= 0) return NRMS_ERR_INVALID_ARG;
   if (int32_t st = shape_ok(w)) return st;
   if (!fused_news_supported(L, w->d_model, w->n_heads, w->query_dim)) return NRMS_ERR_UNSUPPORTED;
@@ -216,7 +234,8 @@ int32_t nrms_news_attention_pool(const float* qkv, int64_t n_rows_qkv, const int
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
   float* wap = cv.floats(fused_news_workspace_floats(n_titles));
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
-  return launch_fused_news(qkv, n_rows_qkv, tok_ids, n_seq_a, tok_ids_b, n_titles, w->w_add,
+  if (ld_qkv == 0) ld_qkv = 3 * (int64_t)w->d_model;
+  return launch_fused_news(qkv, ld_qkv, n_rows_qkv, tok_ids, n_seq_a, tok_ids_b, n_titles, w->w_add,
                            w->b_add, w->q_add, wap, out, stream);
 }
 
@@ -237,6 +256,7 @@ int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const 
   const int D = w->d_model;
   const bool folded = use_folded(proj_mode, n_titles * L, V);
   const NewsSizes z = news_sizes(n_titles, L, V, D, folded);
+  const int64_t ld = news_ld(w, L);
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
   float* qkv = cv.floats(z.qkv);
   float* ctx = cv.floats(z.ctx);
@@ -246,15 +266,15 @@ int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const 
   int32_t st;
   if (folded) {
     // Vocabulary-level projection: one GEMM over the table, then rows gathered by id.
-    st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(w), 3 * D, qkv, 3 * D, stream);
+    st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(w), 3 * D, qkv, ld, stream);
     if (st) return st;
-    return encode_from_qkv(qkv, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
+    return encode_from_qkv(qkv, ld, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
                            stream, wap);
   }
   // Per-token projection with the embedding gather fused into the A-operand load.
-  st = launch_gemm_store(table, V, ids, n_titles * L, D, qkv_rows(w), 3 * D, qkv, 3 * D, stream);
+  st = launch_gemm_store(table, V, ids, n_titles * L, D, qkv_rows(w), 3 * D, qkv, ld, stream);
   if (st) return st;
-  return encode_from_qkv(qkv, n_titles * L, nullptr, n_titles, nullptr, n_titles, L, w, ctx,
+  return encode_from_qkv(qkv, ld, n_titles * L, nullptr, n_titles, nullptr, n_titles, L, w, ctx,
                          scores, out, stream, wap);
 }
 
@@ -266,7 +286,7 @@ size_t nrms_news_encode_folded_workspace_size(int64_t n_titles, int32_t L, int32
 }
 
 int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
-                                const float* qkv_table, int64_t V,
+                                const float* qkv_table, int64_t ld_qkv, int64_t V,
                                 const nrms_encoder_weights_t* w, float* out, void* workspace,
                                 size_t workspace_bytes, hipStream_t stream) {
   if (n_titles < 0 || L <= 0 || V <= 0) return NRMS_ERR_INVALID_ARG;
@@ -279,14 +299,15 @@ int32_t nrms_news_encode_folded(const int64_t* ids, int64_t n_titles, int32_t L,
   float* scores = cv.floats(ntok);
   float* wap = cv.floats(fused_news_workspace_floats(n_titles));
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
-  return encode_from_qkv(qkv_table, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
-                         stream, wap);
+  if (ld_qkv == 0) ld_qkv = 3 * (int64_t)w->d_model;
+  return encode_from_qkv(qkv_table, ld_qkv, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores,
+                         out, stream, wap);
 }
 
 size_t nrms_user_encode_workspace_size(int64_t B, int32_t N, int32_t D) {
   if (B < 0 || N <= 0 || D <= 0) return 0;
   const size_t rows = (size_t)B * N;
-  return align_up(rows * 3 * D * 4) + align_up(rows * D * 4) + align_up(rows * 4) +
+  return align_up(rows * (size_t)qkv_row_stride(D) * 4) + align_up(rows * D * 4) + align_up(rows * 4) +
          align_up(fused_user_packed_b_floats() * 4);
 }
 
@@ -295,7 +316,7 @@ size_t nrms_user_attention_pool_workspace_size(int64_t B, int32_t N, int32_t D) 
   return align_up(fused_user_packed_b_floats() * 4);
 }
 
-int32_t nrms_user_attention_pool(const float* qkv, int64_t B, int32_t N,
+int32_t nrms_user_attention_pool(const float* qkv, int64_t ld_qkv, int64_t B, int32_t N,
                                  const nrms_encoder_weights_t* w, float* out, void* workspace,
                                  size_t workspace_bytes, hipStream_t stream) {
   if (B < 0 || N <= 0) return NRMS_ERR_INVALID_ARG;
@@ -306,7 +327,8 @@ int32_t nrms_user_attention_pool(const float* qkv, int64_t B, int32_t N,
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
   float* wap = cv.floats(fused_user_packed_b_floats());
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
-  return launch_fused_user(qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
+  if (ld_qkv == 0) ld_qkv = 3 * (int64_t)w->d_model;
+  return launch_fused_user(qkv, ld_qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
 }
 
 int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N, int64_t stride_b,
@@ -319,7 +341,8 @@ int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N, int64_t str
   const int D = w->d_model;
   const int64_t rows = B * N;
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
-  float* qkv = cv.floats((size_t)rows * 3 * D);
+  const int64_t ld = user_ld(w, N);
+  float* qkv = cv.floats((size_t)rows * (size_t)ld);
   float* ctx = cv.floats((size_t)rows * D);
   float* scores = cv.floats((size_t)rows);
   float* wap = cv.floats(fused_user_packed_b_floats());
@@ -329,11 +352,11 @@ int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N, int64_t str
   const ARows ar = (stride_b == (int64_t)N * D && stride_n == D) ? contiguous_rows(D)
                                                                  : ARows{N, stride_b, stride_n};
   int32_t st = launch_gemm_store_rows(clicked, rows, ar, nullptr, rows, D, qkv_rows(w), 3 * D, qkv,
-                                      3 * D, stream);
+                                      ld, stream);
   if (st) return st;
   if (fused_user_supported(N, D, w->n_heads, w->query_dim) && ((uintptr_t)out % 16) == 0)
-    return launch_fused_user(qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
-  return encode_from_qkv(qkv, rows, nullptr, B, nullptr, B, N, w, ctx, scores, out, stream);
+    return launch_fused_user(qkv, ld, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
+  return encode_from_qkv(qkv, ld, rows, nullptr, B, nullptr, B, N, w, ctx, scores, out, stream);
 }
 
 int32_t nrms_score(const float* news, int64_t B, int32_t C, int64_t stride_b, int64_t stride_c,
@@ -384,6 +407,7 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   const int64_t n_clk = B * N, n_all = B * (C + N);
   const bool folded = use_folded(proj_mode, n_all * L, V);
   const NewsSizes z = news_sizes(n_all, L, V, D, folded);
+  const int64_t ld = news_ld(news_w, L);
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
   float* qkv = cv.floats(z.qkv);
   float* ctx = cv.floats(z.ctx);
@@ -397,19 +421,19 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
 
   int32_t st;
   if (folded) {
-    st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(news_w), 3 * D, qkv, 3 * D, stream);
+    st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(news_w), 3 * D, qkv, ld, stream);
     if (st) return st;
-    st = encode_from_qkv(qkv, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores, news,
-                         stream, wap);
+    st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
+                         news, stream, wap);
   } else {
-    st = launch_gemm_store(table, V, clicked_ids, n_clk * L, D, qkv_rows(news_w), 3 * D, qkv,
-                           3 * D, stream);
+    st = launch_gemm_store(table, V, clicked_ids, n_clk * L, D, qkv_rows(news_w), 3 * D, qkv, ld,
+                           stream);
     if (st) return st;
     st = launch_gemm_store(table, V, cand_ids, B * C * L, D, qkv_rows(news_w), 3 * D,
-                           qkv + (size_t)n_clk * L * 3 * D, 3 * D, stream);
+                           qkv + (size_t)n_clk * L * ld, ld, stream);
     if (st) return st;
-    st = encode_from_qkv(qkv, n_all * L, nullptr, n_all, nullptr, n_all, L, news_w, ctx, scores,
-                         news, stream, wap);
+    st = encode_from_qkv(qkv, ld, n_all * L, nullptr, n_all, nullptr, n_all, L, news_w, ctx,
+                         scores, news, stream, wap);
   }
   if (st) return st;
   st = nrms_user_encode(news, B, N, (int64_t)N * D, D, user_w, user, user_ws, user_ws_bytes, stream);

@@ -240,7 +240,8 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 // context stored as bf16 planes.
 template <int MODE, bool EXACT>
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
-    const float* __restrict__ qkv, RowMap rmap, int64_t n_groups, const float* __restrict__ WaP,
+    const float* __restrict__ qkv, int64_t ldq, RowMap rmap, int64_t n_groups,
+    const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
     RecheckList rl NRMS_TIMING_PARAM) {
   using Off = QkvOffsets;
@@ -278,7 +279,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   };
   auto store_row = [&](int64_t row, int buf) {
     if (tid < FROWS)
-      rowptr[buf * FROWS + tid] = row >= 0 ? qkv + row * ROW : (row == -1 ? nan_row : zero_row);
+      rowptr[buf * FROWS + tid] = row >= 0 ? qkv + row * ldq : (row == -1 ? nan_row : zero_row);
   };
 
   // attention roles: block b = (title t, head slot hl), lane x within the block
@@ -668,12 +669,13 @@ unsigned long long* g_fused_dbg = nullptr;   // set by profiles/probes/news_vari
 #define NRMS_TIMING_ARG
 #endif
 
-int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a,
+int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s) {
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
+  if (ldq < ROW || ldq % 4) return NRMS_ERR_UNSUPPORTED;   // float4 q / k slices
   const int64_t n_groups = (n_titles + FT - 1) / FT;
   if (4 * n_groups > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   const bool x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6;
@@ -702,12 +704,12 @@ int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a
   }
   const int64_t blocks = n_groups < n_cu ? n_groups : n_cu;   // persistent: one workgroup per CU
   RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows};
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, rm, n_groups, ws,
-                     b_add, q_add, out, rl NRMS_TIMING_ARG);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, n_groups,
+                     ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
   // the recheck pass: reads the count the main pass left; exits at once when 0
   const int64_t blocks_x = blocks < 64 ? blocks : 64;
-  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes, s, qkv, rm,
+  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes, s, qkv, ldq, rm,
                      n_groups, ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
   return launch_status();
 }

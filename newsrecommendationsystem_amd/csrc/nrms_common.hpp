@@ -104,6 +104,13 @@ struct WeightRows {
   int accumulate = 0;  // store GEMMs: Y += X W^T (+ b)
 };
 
+// Row stride (floats) of the q|k|v rows the hot path writes and the fused
+// kernels read: 3D rounded up to 32 floats = whole 128-B lines (928 for
+// D = 300), so no cache line is shared by two GEMM column tiles or two rows
+// (the unpadded 3,600-B rows wrote 1.27x the algorithmic bytes: partial
+// lines at every tile boundary).
+inline int64_t qkv_row_stride(int D) { return ((int64_t)3 * D + 31) / 32 * 32; }
+
 // Process-wide GEMM arithmetic (nrms_set_gemm_arith; defined in capi.hip).
 int gemm_arith();
 
@@ -175,12 +182,13 @@ int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, flo
 
 size_t fused_user_packed_b_floats();
 bool fused_user_supported(int L, int D, int H, int Q);
-int32_t launch_fused_user(const float* qkv, int64_t B, int L, const float* w_add, const float* b_add,
-                          const float* q_add, float* wap, float* out, hipStream_t s);
+int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
+                          const float* b_add, const float* q_add, float* wap, float* out,
+                          hipStream_t s);
 // workspace of launch_fused_news: packed W_add, special rows, recheck list
 size_t fused_news_workspace_floats(int64_t n_titles);
 bool fused_news_supported(int L, int D, int H, int Q);
-int32_t launch_fused_news(const float* qkv, int64_t n_rows, const int64_t* ids_a,
+int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s);

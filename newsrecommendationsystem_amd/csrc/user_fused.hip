@@ -89,7 +89,7 @@ __device__ __forceinline__ int ukpos(int k) {
 
 template <int MODE, int LMAX, int NT>
 __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
-    const float* __restrict__ qkv, int L, const float* __restrict__ WaP,
+    const float* __restrict__ qkv, int64_t ldq, int L, const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out) {
   static_assert(NT >= UH * LMAX, "one (head, query) task per thread");
   constexpr int NW = NT / 64;
@@ -102,14 +102,14 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   const int64_t s = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const float* rows = qkv + s * L * 3 * UD;
+  const float* rows = qkv + s * L * ldq;   // q|k|v rows at stride ldq floats
 
   // ---------------- 0. stage K|V (all loads in flight at once), q slices ----------------
   const bool has = tid < UH * L;
   const int h = has ? tid / L : 0, qi = has ? tid - h * L : 0;
   float q[UDK];
   {
-    const float4* qp = reinterpret_cast<const float4*>(rows + (size_t)qi * 3 * UD + UDK * h);
+    const float4* qp = reinterpret_cast<const float4*>(rows + (size_t)qi * ldq + UDK * h);
 #pragma unroll
     for (int t = 0; t < UDK / 4; ++t) {
       const float4 v = qp[t];
@@ -122,7 +122,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     for (int k = 0; k < PER; ++k) {
       const int e = tid + k * NT;
       const int i = e / KV4, c = e - i * KV4;
-      buf[k] = e < L * KV4 ? *reinterpret_cast<const float4*>(rows + (size_t)i * 3 * UD + UD + 4 * c)
+      buf[k] = e < L * KV4 ? *reinterpret_cast<const float4*>(rows + (size_t)i * ldq + UD + 4 * c)
                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
@@ -372,22 +372,22 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 }
 
 template <int MODE, int LMAX, int NT>
-int32_t launch_user_inst(const float* qkv, int64_t B, int L, const float* wap, const float* b_add,
-                         const float* q_add, float* out, hipStream_t s) {
+int32_t launch_user_inst(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
+                         const float* b_add, const float* q_add, float* out, hipStream_t s) {
   const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64) * 4;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>), (int)lds);
   hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
-                     L, wap, b_add, q_add, out);
+                     ldq, L, wap, b_add, q_add, out);
   return launch_status();
 }
 
 template <int MODE>
-int32_t launch_user_mode(const float* qkv, int64_t B, int L, const float* wap, const float* b_add,
-                         const float* q_add, float* out, hipStream_t s) {
-  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, B, L, wap, b_add, q_add, out, s);
-  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, B, L, wap, b_add, q_add, out, s);
-  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, B, L, wap, b_add, q_add, out, s);
-  return launch_user_inst<MODE, 64, 1024>(qkv, B, L, wap, b_add, q_add, out, s);
+int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
+                         const float* b_add, const float* q_add, float* out, hipStream_t s) {
+  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
+  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
+  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
+  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
 }
 
 }  // namespace
@@ -398,17 +398,19 @@ bool fused_user_supported(int L, int D, int H, int Q) {
   return L >= 1 && L <= 64 && D == UD && H == UH && Q == UQ;
 }
 
-int32_t launch_fused_user(const float* qkv, int64_t B, int L, const float* w_add, const float* b_add,
-                          const float* q_add, float* wap, float* out, hipStream_t s) {
+int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
+                          const float* b_add, const float* q_add, float* wap, float* out,
+                          hipStream_t s) {
   if (B == 0) return NRMS_OK;
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
-  if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16) return NRMS_ERR_UNSUPPORTED;
+  if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16 || ldq < 3 * UD || ldq % 4)
+    return NRMS_ERR_UNSUPPORTED;
   const int x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6 ? 1 : 0;
   const int npk = x6 ? UKS * UNT * 64 * 8 : UWAP1;
   hipLaunchKernelGGL(pack_user_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap, x6);
   if (int32_t st = launch_status()) return st;
-  if (x6) return launch_user_mode<1>(qkv, B, L, wap, b_add, q_add, out, s);
-  return launch_user_mode<0>(qkv, B, L, wap, b_add, q_add, out, s);
+  if (x6) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
+  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
 }
 
 }  // namespace nrms

@@ -135,8 +135,9 @@ class NewsEncoder(nn.Module):
         tab = self.table()
         V, D = tab.shape
         w, keep = self.weights()
-        qkv = torch.empty(V, 3 * D, dtype=torch.float32, device=tab.device)
-        N.call("nrms_qkv_project", N.ptr(tab), V, None, V, ctypes_byref(w), N.ptr(qkv),
+        ld = N.load().nrms_qkv_row_stride(D)   # rows padded to whole 128-B lines
+        qkv = torch.empty(V, ld, dtype=torch.float32, device=tab.device)
+        N.call("nrms_qkv_project", N.ptr(tab), V, None, V, ctypes_byref(w), N.ptr(qkv), ld,
                N.stream_handle(tab.device))
         self._folded = (key, qkv)
         return qkv
@@ -159,7 +160,8 @@ class NewsEncoder(nn.Module):
             qkv = self.folded_table()
             nb = N.load().nrms_news_encode_folded_workspace_size(n, L, D)
             ws = self._ws.get(nb, tab.device)
-            N.call("nrms_news_encode_folded", N.ptr(ids), n, L, N.ptr(qkv), V, ctypes_byref(w),
+            N.call("nrms_news_encode_folded", N.ptr(ids), n, L, N.ptr(qkv), qkv.shape[1], V,
+                   ctypes_byref(w),
                    N.ptr(out), N.ptr(ws), ws.numel(), stream)
         else:
             nb = N.load().nrms_news_encode_workspace_size(n, L, V, D, mode)

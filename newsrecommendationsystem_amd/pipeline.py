@@ -42,11 +42,15 @@ class ForwardPlan:
         f32 = dict(dtype=torch.float32, device=self.dev)
         D = self.D
         qkv_rows = self.V if self.folded else n_all * L
-        self.qkv = torch.empty(qkv_rows, 3 * D, **f32)
+        lib = N.load()
+        # the fused tails read rows padded to whole 128-B lines; the stage kernels packed rows
+        self.ldq = lib.nrms_qkv_row_stride(D) if fused else 3 * D
+        self.uldq = lib.nrms_qkv_row_stride(D) if fused and n_clicked <= 64 else 3 * D
+        self.qkv = torch.empty(qkv_rows, self.ldq, **f32)
         self.ctx = torch.empty(n_all * L, D, **f32)
         self.scores = torch.empty(n_all * L, **f32)
         self.news = torch.empty(n_all, D, **f32)        # [clicked B*N | candidates B*C]
-        self.uqkv = torch.empty(B * n_clicked, 3 * D, **f32)
+        self.uqkv = torch.empty(B * n_clicked, self.uldq, **f32)
         self.uctx = torch.empty(B * n_clicked, D, **f32)
         self.uscores = torch.empty(B * n_clicked, **f32)
         self.user = torch.empty(B, D, **f32)
@@ -54,7 +58,6 @@ class ForwardPlan:
         self.wn, self._keep_n = ne.weights()
         self.wu, self._keep_u = model.user_encoder.weights()
         self.fused = fused
-        lib = N.load()
         self.user_fused = fused and n_clicked <= 64 and D == D_MODEL
         news_st = ["news_fused"] if fused else ["mhsa_news", "addscore_news", "pool_news"]
         user_st = ["user_fused"] if self.user_fused else ["mhsa_user", "addscore_user", "pool_user"]
@@ -78,18 +81,20 @@ class ForwardPlan:
         rec = (lambda i: events[i].record()) if events is not None else (lambda i: None)
 
         rec(0)
+        ldq, uldq = self.ldq, self.uldq
         if self.folded:
-            N.call("nrms_qkv_project", P(self.table), V, None, V, wn, P(self.qkv), st)
+            N.call("nrms_qkv_project", P(self.table), V, None, V, wn, P(self.qkv), ldq, st)
         else:
             N.call("nrms_qkv_project", P(self.table), V, P(clicked_ids), n_clk * L, wn,
-                   P(self.qkv), st)
+                   P(self.qkv), ldq, st)
             tail = self.qkv[n_clk * L:]
-            N.call("nrms_qkv_project", P(self.table), V, P(cand_ids), B * C * L, wn, P(tail), st)
+            N.call("nrms_qkv_project", P(self.table), V, P(cand_ids), B * C * L, wn, P(tail), ldq,
+                   st)
         rec(1)
         k = 1
         rows, ia, ib = (V, P(clicked_ids), P(cand_ids)) if self.folded else (n_all * L, None, None)
         if self.fused:
-            N.call("nrms_news_attention_pool", P(self.qkv), rows, ia, n_clk, ib, n_all, L, wn,
+            N.call("nrms_news_attention_pool", P(self.qkv), ldq, rows, ia, n_clk, ib, n_all, L, wn,
                    P(self.news), P(self.fws), self.fws.numel(), st)
         else:
             N.call("nrms_self_attention", P(self.qkv), rows, ia, n_clk, ib, n_all, L, wn,
@@ -101,11 +106,11 @@ class ForwardPlan:
             k += 2
         k += 1
         rec(k)
-        N.call("nrms_qkv_project", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), st)
+        N.call("nrms_qkv_project", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), uldq, st)
         rec(k + 1)
         if self.user_fused:
-            N.call("nrms_user_attention_pool", P(self.uqkv), B, Nc, wu, P(self.user), P(self.uws),
-                   self.uws.numel(), st)
+            N.call("nrms_user_attention_pool", P(self.uqkv), uldq, B, Nc, wu, P(self.user),
+                   P(self.uws), self.uws.numel(), st)
             k += 1
         else:
             N.call("nrms_self_attention", P(self.uqkv), n_clk, None, B, None, B, Nc, wu,

@@ -90,7 +90,7 @@ class NRMSTrain(torch.autograd.Function):
         N.call("nrms_dropout", P(X), P(Xd), R * D, ctypes.c_float(p), ctypes.c_uint64(s1), st)
         del X
         qkv = torch.empty(R, 3 * D, **f32)
-        N.call("nrms_qkv_project", P(Xd), R, None, R, ewn, P(qkv), st)
+        N.call("nrms_qkv_project", P(Xd), R, None, R, ewn, P(qkv), 0, st)
         cm = torch.empty(R, D, **f32)
         N.call("nrms_self_attention", P(qkv), R, None, T, None, T, L, ewn, P(cm), st)
         cd = torch.empty_like(cm)
@@ -104,7 +104,7 @@ class NRMSTrain(torch.autograd.Function):
 
         Ru = B * n_clk
         uqkv = torch.empty(Ru, 3 * D, **f32)
-        N.call("nrms_qkv_project", P(clk_vec), Ru, None, Ru, ewu, P(uqkv), st)
+        N.call("nrms_qkv_project", P(clk_vec), Ru, None, Ru, ewu, P(uqkv), 0, st)
         uctx = torch.empty(Ru, D, **f32)
         N.call("nrms_self_attention", P(uqkv), Ru, None, B, None, B, n_clk, ewu, P(uctx), st)
         yu = torch.empty(Ru, Q, **f32)

@@ -46,13 +46,16 @@ def main():
         P = N.ptr
         wn, wu = ctypes.byref(plan.wn), ctypes.byref(plan.wu)
         calls = {
-            "qkv_news": lambda: N.call("nrms_qkv_project", P(plan.table), V, None, V, wn, P(plan.qkv), st),
-            "news_fused": lambda: N.call("nrms_news_attention_pool", P(plan.qkv), V, P(clk), n_clk, P(cand),
-                                         n_all, L, wn, P(plan.news), P(plan.fws), plan.fws.numel(), st),
+            "qkv_news": lambda: N.call("nrms_qkv_project", P(plan.table), V, None, V, wn, P(plan.qkv),
+                                       plan.ldq, st),
+            "news_fused": lambda: N.call("nrms_news_attention_pool", P(plan.qkv), plan.ldq, V, P(clk), n_clk,
+                                         P(cand), n_all, L, wn, P(plan.news), P(plan.fws),
+                                         plan.fws.numel(), st),
             "mhsa_news": lambda: N.call("nrms_self_attention", P(plan.qkv), V, P(clk), n_clk, P(cand), n_all,
                                         L, wn, P(plan.ctx), st),
             "addscore_news": lambda: N.call("nrms_additive_scores", P(plan.ctx), n_all * L, wn, P(plan.scores), st),
-            "qkv_user": lambda: N.call("nrms_qkv_project", P(plan.news), n_clk, None, n_clk, wu, P(plan.uqkv), st),
+            "qkv_user": lambda: N.call("nrms_qkv_project", P(plan.news), n_clk, None, n_clk, wu, P(plan.uqkv),
+                                       plan.uldq, st),
             "mhsa_user": lambda: N.call("nrms_self_attention", P(plan.uqkv), n_clk, None, B, None, B, Nc, wu,
                                         P(plan.uctx), st),
         }

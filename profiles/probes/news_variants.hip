@@ -76,12 +76,12 @@ int main(int argc, char** argv) {
     nrms::g_arith = var ? NRMS_GEMM_SPLIT_BF16X6 : NRMS_GEMM_F32;
     float* out = outs[var];
     for (int it = 0; it < 2; ++it)
-      if (nrms::launch_fused_news(qkv, V, ids, n_titles, nullptr, n_titles, wa, b, q, wap, out, 0)) return 2;
+      if (nrms::launch_fused_news(qkv, 900, V, ids, n_titles, nullptr, n_titles, wa, b, q, wap, out, 0)) return 2;
     CK(hipDeviceSynchronize());
     CK(hipMemset(dbg, 0, 256 * 8 * 8 * 8));
     CK(hipEventRecord(e0, 0));
     for (int it = 0; it < reps; ++it)
-      if (nrms::launch_fused_news(qkv, V, ids, n_titles, nullptr, n_titles, wa, b, q, wap, out, 0)) return 2;
+      if (nrms::launch_fused_news(qkv, 900, V, ids, n_titles, nullptr, n_titles, wa, b, q, wap, out, 0)) return 2;
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;

@@ -42,7 +42,7 @@ def main():
 
     # plain GEMM check with structured data: X = arange pattern, W identity-ish
     qkv = torch.empty(n * L, 900, device=dev)
-    N.call("nrms_qkv_project", P(tab), V, P(ids), n * L, ctypes.byref(w), P(qkv), st)
+    N.call("nrms_qkv_project", P(tab), V, P(ids), n * L, ctypes.byref(w), P(qkv), 0, st)
     torch.cuda.synchronize()
     x = sd["news_encoder.word_embedding.weight"][ids_np].reshape(-1, 300)
     p = "news_encoder.multihead_self_attention"
@@ -60,7 +60,7 @@ def main():
                           keep[6].data_ptr(), keep[7].data_ptr(), keep[8].data_ptr(), 300, 15, 200)
     X = (torch.arange(300 * 256, device=dev, dtype=torch.float32).view(256, 300) % 97) / 97.0
     Y = torch.empty(256, 900, device=dev)
-    N.call("nrms_qkv_project", P(X), 256, None, 256, ctypes.byref(w2), P(Y), st)
+    N.call("nrms_qkv_project", P(X), 256, None, 256, ctypes.byref(w2), P(Y), 0, st)
     torch.cuda.synchronize()
     Yn = Y.cpu().numpy()
     Xn = X.cpu().numpy()

@@ -285,7 +285,9 @@ def test_fused_news_tail_vs_stages(device, n, gemm_mode):
     sd = W.nrms_state(21, V)
     m = _module(sd, V, device, hip_cache_folded_table=False)
     ne = m.news_encoder
-    qkv = ne.folded_table()
+    qkv = ne.folded_table()                     # rows padded to nrms_qkv_row_stride
+    packed = qkv[:, :900].contiguous()          # the stage kernels' packed layout
+    assert qkv.shape[1] == N.load().nrms_qkv_row_stride(300) == 928
     ids = torch.from_numpy(W.titles(21, 40 + n, n, V, min_len=1)).to(device)
     na = n // 2
     # a NULL first id array means "identity rows" in the ABI, so never pass an empty one
@@ -295,12 +297,16 @@ def test_fused_news_tail_vs_stages(device, n, gemm_mode):
     out = torch.empty(n, 300, device=device)
     nb = N.load().nrms_news_attention_pool_workspace_size(n, 20, 300)
     ws = torch.empty(nb, dtype=torch.uint8, device=device)
-    N.call("nrms_news_attention_pool", N.ptr(qkv), V, N.ptr(ia), na, N.ptr(ib), n, 20,
+    N.call("nrms_news_attention_pool", N.ptr(qkv), qkv.shape[1], V, N.ptr(ia), na, N.ptr(ib), n, 20,
            ctypes.byref(w), N.ptr(out), N.ptr(ws), nb, st)
+    out900 = torch.empty(n, 300, device=device)     # same rows at stride 900: bitwise equal
+    N.call("nrms_news_attention_pool", N.ptr(packed), 900, V, N.ptr(ia), na, N.ptr(ib), n, 20,
+           ctypes.byref(w), N.ptr(out900), N.ptr(ws), nb, st)
+    assert torch.equal(out, out900)
     ctx = torch.empty(n * 20, 300, device=device)
     sc = torch.empty(n * 20, device=device)
     ref = torch.empty(n, 300, device=device)
-    N.call("nrms_self_attention", N.ptr(qkv), V, N.ptr(ia), na, N.ptr(ib), n, 20, ctypes.byref(w),
+    N.call("nrms_self_attention", N.ptr(packed), V, N.ptr(ia), na, N.ptr(ib), n, 20, ctypes.byref(w),
            N.ptr(ctx), st)
     N.call("nrms_additive_attention", N.ptr(ctx), n, 20, ctypes.byref(w), N.ptr(sc), N.ptr(ref), st)
     err = ((out - ref).norm(dim=1) / ref.norm(dim=1)).max()
@@ -348,7 +354,7 @@ def test_stage_abi_matches_module(golden, golden_state, device):
     sc = torch.empty(n * L, device=device)
     out = torch.empty(n, 300, device=device)
     N.call("nrms_qkv_project", N.ptr(tab), tab.shape[0], N.ptr(ids), n * L, ctypes.byref(w),
-           N.ptr(qkv), st)
+           N.ptr(qkv), 0, st)
     N.call("nrms_self_attention", N.ptr(qkv), n * L, None, n, None, n, L, ctypes.byref(w),
            N.ptr(ctx), st)
     N.call("nrms_additive_attention", N.ptr(ctx), n, L, ctypes.byref(w), N.ptr(sc), N.ptr(out), st)
@@ -359,7 +365,7 @@ def test_stage_abi_matches_module(golden, golden_state, device):
     fused = torch.empty(n, 300, device=device)
     nb = N.load().nrms_news_attention_pool_workspace_size(n, L, 300)
     ws = torch.empty(nb, dtype=torch.uint8, device=device)
-    N.call("nrms_news_attention_pool", N.ptr(qkv), n * L, None, n, None, n, L, ctypes.byref(w),
+    N.call("nrms_news_attention_pool", N.ptr(qkv), 0, n * L, None, n, None, n, L, ctypes.byref(w),
            N.ptr(fused), N.ptr(ws), nb, st)
     assert torch.equal(fused, ref)
     assert O.normwise_rel_err(_np(fused), golden["news_out"]).max() < TOL
@@ -433,12 +439,13 @@ def test_fused_user_tail_vs_stages(device, B, n_clk, gemm_mode):
     st = N.stream_handle(device)
     lib = N.load()
     uqkv = torch.empty(B * n_clk, 900, device=device)
-    N.call("nrms_qkv_project", N.ptr(x), B * n_clk, None, B * n_clk, ctypes.byref(w), N.ptr(uqkv), st)
+    N.call("nrms_qkv_project", N.ptr(x), B * n_clk, None, B * n_clk, ctypes.byref(w), N.ptr(uqkv), 0,
+           st)
     out = torch.empty(B, 300, device=device)
     nb = lib.nrms_user_attention_pool_workspace_size(B, n_clk, 300)
     ws = torch.empty(nb, dtype=torch.uint8, device=device)
-    N.call("nrms_user_attention_pool", N.ptr(uqkv), B, n_clk, ctypes.byref(w), N.ptr(out), N.ptr(ws),
-           nb, st)
+    N.call("nrms_user_attention_pool", N.ptr(uqkv), 0, B, n_clk, ctypes.byref(w), N.ptr(out),
+           N.ptr(ws), nb, st)
     ctx = torch.empty(B * n_clk, 300, device=device)
     sc = torch.empty(B * n_clk, device=device)
     ref = torch.empty(B, 300, device=device)
@@ -470,7 +477,7 @@ def test_user_tail_beyond_fused_range(device, n_clk):
     lib = N.load()
     out = torch.empty(B, 300, device=device)
     x = torch.zeros(B * n_clk, 900, device=device)
-    rc = lib.nrms_user_attention_pool(N.ptr(x), B, n_clk, ctypes.byref(w), N.ptr(out), None, 0,
+    rc = lib.nrms_user_attention_pool(N.ptr(x), 0, B, n_clk, ctypes.byref(w), N.ptr(out), None, 0,
                                       N.stream_handle(device))
     assert rc == N.NRMS_ERR_UNSUPPORTED
     with torch.no_grad():
