@@ -357,7 +357,17 @@ def main():
         for i, st in enumerate(plan.stages):
             stage_ms[st] += ev[i].elapsed_time(ev[i + 1])
     stage_ms = {st: v / steps for st, v in stage_ms.items()}
-    work = plan.work()
+    # titles the news tail encodes per step: with padding-title dedupe (library
+    # default, nrms_set_title_dedupe) all-zero titles count once
+    # (nrms_forward orders titles [clicked | candidates]; whole 4-title groups of
+    # padding are skipped, one of them encoded)
+    all_titles = torch.cat([clk.reshape(-1, L), cand.reshape(-1, L)])
+    n_titles = all_titles.shape[0]
+    n_pad = int((all_titles == 0).all(-1).sum())
+    grp = torch.nn.functional.pad((all_titles != 0).any(-1), (0, (-n_titles) % 4)).view(-1, 4).any(-1)
+    n_pad_groups = int((~grp).sum())
+    n_enc = 4 * (grp.numel() - n_pad_groups + (1 if n_pad_groups else 0))
+    work = plan.work(titles_encoded=n_enc)
     dom = max(stage_ms, key=stage_ms.get)
     w = work[dom]
     t_dom = stage_ms[dom] / 1e3
@@ -415,6 +425,11 @@ def main():
                               "users": S.N_USERS, "sharding": "user_id % world"},
                    "parallelism": f"user-shard x{world}"},
         "roofline": roofline,
+        "titles": {"per_step": n_titles, "all_padding": n_pad, "all_padding_groups": n_pad_groups,
+                   "encoded": n_enc,
+                   "dedupe": "one all-padding 4-title group encoded per step, its slot vectors "
+                             "copied to the other all-padding groups (bitwise identical logits; "
+                             "no_title_dedupe below times every title encoded)"},
         "stages_ms": {st: round(v, 4) for st, v in stage_ms.items()},
         "plan_equals_nrms_forward": same,
     }
@@ -427,6 +442,18 @@ def main():
             with torch.no_grad():
                 dplan.run(cand, clk)
                 dms = _time_launches(lambda: dplan.run(cand, clk), 10, device)
+            lib = Nat.load()
+            lib.nrms_set_title_dedupe(0)
+            try:
+                with torch.no_grad():
+                    plan.run(cand, clk)
+                    nms = _time_launches(lambda: plan.run(cand, clk), 10, device)
+            finally:
+                lib.nrms_set_title_dedupe(1)
+            out["no_title_dedupe"] = {
+                "ms_per_step": round(nms, 4), "impressions_per_s": round(B / (nms / 1e3), 1),
+                "note": "every all-padding history title encoded separately (nrms_set_title_dedupe(0)), "
+                        "bitwise the same logits"}
             out["direct_projection"] = {
                 "ms_per_step": round(dms, 4), "impressions_per_s": round(B / (dms / 1e3), 1),
                 "note": "per-token Q|K|V projection (no vocabulary folding): the work SURVEY §8d's "

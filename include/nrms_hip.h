@@ -92,6 +92,16 @@ typedef enum { NRMS_GEMM_SPLIT_BF16X6 = 0, NRMS_GEMM_F32 = 1 } nrms_gemm_arith_t
 int32_t nrms_set_gemm_arith(int32_t mode);
 int32_t nrms_get_gemm_arith(void);
 
+/* All-padding titles (20 zero ids: the left-padding of short histories,
+ * src/dataset.py:79-83, ~45 % of the clicked slots at BASELINE config 3) all
+ * have the same news vector. With dedupe on (default), the fused news tail
+ * encodes one of them per call and copies its vector to the others; every
+ * output is bitwise the same as encoding each title (a title's vector depends
+ * on its own ids only). Applies where ids are passed (folded projection).
+ * Process-wide, read at enqueue time; returns the previous setting.
+ * NRMS_DEDUPE=0 in the environment starts with it off. */
+int32_t nrms_set_title_dedupe(int32_t on);
+
 int32_t nrms_abi_version(void);
 const char* nrms_status_string(int32_t status);
 int32_t nrms_last_hip_error(void);

@@ -38,6 +38,7 @@ _EW = ctypes.POINTER(EncoderWeights)
 SIGNATURES = {
     "nrms_abi_version": (_i32, []),
     "nrms_set_gemm_arith": (_i32, [_i32]),
+    "nrms_set_title_dedupe": (_i32, [_i32]),
     "nrms_get_gemm_arith": (_i32, []),
     "nrms_status_string": (ctypes.c_char_p, [_i32]),
     "nrms_last_hip_error": (_i32, []),

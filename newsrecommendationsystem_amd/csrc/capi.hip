@@ -143,6 +143,8 @@ int32_t nrms_set_gemm_arith(int32_t mode) {
 
 int32_t nrms_get_gemm_arith(void) { return gemm_arith(); }
 
+int32_t nrms_set_title_dedupe(int32_t on) { return set_title_dedupe(on); }
+
 const char* nrms_status_string(int32_t st) {
   switch (st) {
     case NRMS_OK: return "ok";

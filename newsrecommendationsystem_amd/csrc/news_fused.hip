@@ -38,6 +38,8 @@
 // (M-tile 4, N-tile 12).
 #include "nrms_common.hpp"
 
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 namespace nrms {
@@ -103,7 +105,8 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
                                                               float* __restrict__ WaP,
                                                               int32_t* __restrict__ recheck_count) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx == 0) *recheck_count = 0;
+  if (idx < 4)   // [recheck count, group-list count, rep, 0]
+    recheck_count[idx] = idx == 2 ? INT32_MAX : 0;
   if (idx >= WAP_FLOATS + SPECIAL_FLOATS) return;
   if (idx >= WAP_FLOATS) {
     const int sidx = idx - WAP_FLOATS;
@@ -125,7 +128,7 @@ __global__ __launch_bounds__(256) void pack_additive_b3_kernel(const float* __re
                                                                float* __restrict__ WaP,
                                                                int32_t* __restrict__ recheck_count) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx == 0) *recheck_count = 0;
+  if (idx < 4) recheck_count[idx] = idx == 2 ? INT32_MAX : 0;
   constexpr int NE = XKS * FNT * 64 * 8;
   if (idx >= NE + SPECIAL_FLOATS) return;
   if (idx >= NE) {
@@ -144,6 +147,7 @@ __global__ __launch_bounds__(256) void pack_additive_b3_kernel(const float* __re
   o[2 * 64 * 8] = lo;
 }
 
+
 struct RowMap {
   const int64_t* ids_a;
   const int64_t* ids_b;
@@ -156,7 +160,78 @@ struct RowMap {
     const int64_t id = ids[i];
     return ((uint64_t)id < (uint64_t)n_rows) ? id : -1;
   }
+  __device__ __forceinline__ const int64_t* ids_of(int64_t s) const {
+    return (s < n_seq_a || ids_b == nullptr) ? ids_a + s * FL : ids_b + (s - n_seq_a) * FL;
+  }
 };
+
+// Groups the main pass encodes. Every all-padding title (20 zero ids: the
+// left-padding of short histories, src/dataset.py:79-83) has the same news
+// vector in a given slot of its 4-title group, and padding runs are contiguous
+// (histories are left-padded), so whole groups are padding. With a list, the
+// main pass encodes only the groups holding a real title, plus one
+// all-padding group (rep, the lowest); broadcast_padding_kernel then copies
+// rep's vector of slot s % 4 to every title s of the other all-padding groups.
+// Groups keep their titles and slots, so every output is bitwise the one the
+// undeduplicated launch computes (a row's additive score sums its N-tile
+// partials in an order set by its slot); the list order (atomics) only
+// decides which workgroup encodes which group. Without a list group k is k.
+struct GroupList {
+  const int32_t* list;
+  const int32_t* count;
+  const int32_t* rep;   // INT32_MAX: no all-padding group
+};
+
+// One thread per group: classify (all 80 ids zero; slots past n_titles count as
+// padding) and append the others to the list; one atomic per wave (vector
+// atomics only).
+__global__ __launch_bounds__(256) void classify_groups_kernel(RowMap rm, int64_t n_groups,
+                                                              int32_t* __restrict__ list,
+                                                              int32_t* __restrict__ count,
+                                                              int32_t* __restrict__ rep,
+                                                              uint8_t* __restrict__ pad_group) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool live = g < n_groups;
+  bool pad = false;
+  if (live) {
+    int64_t any = 0;
+    for (int t = 0; t < FT; ++t) {
+      const int64_t s = g * FT + t;
+      if (s >= rm.n_titles) break;
+      const int64_t* ids = rm.ids_of(s);
+#pragma unroll
+      for (int i = 0; i < FL; i += 2) {
+        const int4 v = *reinterpret_cast<const int4*>(ids + i);   // 16-B aligned id rows (checked)
+        any |= (int64_t)(v.x | v.y | v.z | v.w);
+      }
+    }
+    pad = any == 0;
+    pad_group[g] = pad ? 1 : 0;
+  }
+  const uint64_t keep = __ballot(live && !pad);
+  const uint64_t pads = __ballot(live && pad);
+  int base = 0;
+  if (lane == 0 && keep) base = atomicAdd(count, __popcll(keep));
+  base = __shfl(base, 0);
+  if (live && !pad) list[base + __popcll(keep & ((1ull << lane) - 1))] = (int32_t)g;
+  if (pads != 0 && lane == 0)
+    atomicMin(rep, (int32_t)((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63) + __ffsll((long long)pads) - 1));
+}
+
+// out[s] = out[4 rep + s % 4] for every title s of the other all-padding groups.
+__global__ __launch_bounds__(256) void broadcast_padding_kernel(const uint8_t* __restrict__ pad_group,
+                                                                const int32_t* __restrict__ rep,
+                                                                int64_t n_titles, float* __restrict__ out) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (title, float4 column)
+  const int64_t s = t / (FD / 4);
+  if (s >= n_titles || !pad_group[s / FT]) return;
+  const int64_t r = *rep;
+  if (s / FT == r) return;
+  const int c = (int)(t - s * (FD / 4));
+  reinterpret_cast<float4*>(out + s * FD)[c] =
+      reinterpret_cast<const float4*>(out + (r * FT + (s % FT)) * FD)[c];
+}
 
 // Rows near fp32 overflow (nrms_common.hpp, kExpRecheck). The main pass
 // (EXACT = false) takes the fast exp everywhere and appends the title groups
@@ -240,7 +315,7 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 // context stored as bf16 planes.
 template <int MODE, bool EXACT>
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
-    const float* __restrict__ qkv, int64_t ldq, RowMap rmap, int64_t n_groups,
+    const float* __restrict__ qkv, int64_t ldq, RowMap rmap, GroupList gl,
     const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
     RecheckList rl NRMS_TIMING_PARAM) {
@@ -249,7 +324,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* ctxL = lds;                                   // f32: [80][SC]
   __bf16* ctxB = reinterpret_cast<__bf16*>(lds);       // x6:  [80][XRB] = hi | mid | lo planes
-  float* part = X6 ? lds + FROWS * XRB / 2 : ctxL + FROWS * SC;   // [4][80] per-wave row partials
+  float* part = X6 ? lds + FROWS * XRB / 2 : ctxL + FROWS * SC;   // [80][4] per-wave row partials
   const float** rowptr = reinterpret_cast<const float**>(part + 4 * FROWS);   // [2][80]
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -272,6 +347,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   // row pointers of title group tg -> rowptr[buf]: the token id is loaded by
   // row_of (threads < 80), the pointer stored later by store_row, so the id
   // load's latency hides behind the work in between.
+  const int64_t n_groups = (rmap.n_titles + FT - 1) / FT;
   auto row_of = [&](int64_t tg) -> int64_t {
     if (tid >= FROWS) return -2;
     const int t = tid / FL;
@@ -342,9 +418,13 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   // iteration k of this workgroup handles title group group_at(k): k itself in
   // the main pass, the k-th flagged group in the EXACT pass (past the end: a
   // group of padding titles, so the prefetch of "the next group" stays valid)
-  const int64_t n_iter = EXACT ? (int64_t)*rl.count : n_groups;
+  // (main pass with a group list: the listed groups, then rep)
+  const int64_t n_list = gl.list ? (int64_t)*gl.count : n_groups;
+  const int32_t rep = gl.list ? *gl.rep : INT32_MAX;
+  const int64_t n_iter = EXACT ? (int64_t)*rl.count : n_list + (rep != INT32_MAX ? 1 : 0);
   auto group_at = [&](int64_t k) -> int64_t {
     if constexpr (EXACT) return k < n_iter ? (int64_t)rl.list[k] : n_groups;
+    if (gl.list) return k < n_list ? (int64_t)gl.list[k] : (k == n_list && rep != INT32_MAX ? (int64_t)rep : n_groups);
     else return k;
   };
   if (blockIdx.x < n_iter) store_row(row_of(group_at(blockIdx.x)), 0);
@@ -480,28 +560,32 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         for (int j = 0; j < 3; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
       if constexpr (X6) {
         // A fragments (16x16x32): lane holds A[row lm][32 ks + 8 kq .. + 7] of each plane
-        const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
         const __bf16* Ab = ctxB + lm * XRB + 8 * kq;
+        const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
+        // plane-major: the hi planes (first product's B) arrive first
         auto load_b = [&](int ks, bf16x8 (&dst)[4][3]) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const int nt = j < 3 ? 3 * w + j : 12;
+          for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl) dst[j][pl] = Bq[((ks * FNT + nt) * 3 + pl) * 64];
-          }
+            for (int j = 0; j < 4; ++j) {
+              const int nt = j < 3 ? 3 * w + j : 12;
+              dst[j][pl] = Bq[((ks * FNT + nt) * 3 + pl) * 64];
+            }
         };
         // one 32-deep k-step; EXTRA: wave 0 also owns (M-tile 4, N-tile 12)
-        auto kstep = [&](int ks, const bf16x8 (&bb)[4][3], auto extra) {
-          constexpr bool EXTRA = decltype(extra)::value;
-          bf16x8 a[FMT][3], ax[3];
+        // the wave index is a template constant (the X tile's A rows = M-tile
+        // W: no second read of them); A planes loaded lo first, the order the
+        // products consume them
+        auto kstep = [&](int ks, const bf16x8 (&bb)[4][3], auto wc) {
+          constexpr int W = decltype(wc)::value;
+          constexpr bool EXTRA = W == 0;
+          bf16x8 a[FMT][3];
 #pragma unroll
-          for (int mt = 0; mt < FMT; ++mt)
+          for (int pl = 2; pl >= 0; --pl)
 #pragma unroll
-            for (int pl = 0; pl < 3; ++pl)
+            for (int mt = 0; mt < FMT; ++mt)
               a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * XRB + pl * XKP + 32 * ks);
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
-            ax[pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * w * XRB + pl * XKP + 32 * ks);
+          const bf16x8 (&ax)[3] = a[W];
           // the six products with i + j <= 2, smallest first
 #define NRMS_X6STEP(PA, PB)                                                                              \
   _Pragma("unroll") for (int mt = 0; mt < FMT; ++mt)                                                     \
@@ -525,8 +609,12 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           }
         };
         static_assert(XKS % 2 == 0, "k-steps in pairs");
-        if (w == 0) mainloop(std::true_type{});
-        else mainloop(std::false_type{});
+        switch (w) {
+          case 0: mainloop(std::integral_constant<int, 0>{}); break;
+          case 1: mainloop(std::integral_constant<int, 1>{}); break;
+          case 2: mainloop(std::integral_constant<int, 2>{}); break;
+          default: mainloop(std::integral_constant<int, 3>{}); break;
+        }
       } else {
       float4 bb[4], bn[4];
 #pragma unroll
@@ -644,19 +732,28 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     NRMS_STAMP(6)
   }
 #ifdef NRMS_FUSED_TIMING
-  if (lane == 0)
+  if (!EXACT && lane == 0)
     for (int k = 0; k < 8; ++k) dbg[(blockIdx.x * 4 + w) * 8 + k] = tacc[k];
 #endif
 }
 
 }  // namespace
 
-// packed W_add + special rows, then the recheck counter and list (int32)
+// packed W_add + special rows, then int32 [recheck count, group-list count,
+// rep, 0], the recheck list (4 per group), the group list, pad_group bytes
 static size_t fused_news_list_offset() { return (size_t)WAP_MAX + SPECIAL_FLOATS; }
 size_t fused_news_workspace_floats(int64_t n_titles) {
   const int64_t n_groups = (n_titles + FT - 1) / FT;
-  return fused_news_list_offset() + 4 + 4 * (size_t)n_groups;
+  return fused_news_list_offset() + 4 + 4 * (size_t)n_groups + (size_t)n_groups +
+         ((size_t)n_groups + 3) / 4;
 }
+
+static std::atomic<int> g_title_dedupe{[] {
+  const char* e = getenv("NRMS_DEDUPE");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
+int title_dedupe() { return g_title_dedupe.load(std::memory_order_relaxed); }
+int set_title_dedupe(int on) { return g_title_dedupe.exchange(on ? 1 : 0); }
 
 bool fused_news_supported(int L, int D, int H, int Q) {
   return L == FL && D == FD && H == FH && Q == FQ;
@@ -686,6 +783,12 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   ensure_dynamic_lds(reinterpret_cast<const void*>(kern_exact), (int)lds_bytes);
   int32_t* rcount = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
   const RecheckList rl{rcount, rcount + 4};
+  int32_t* glist = rcount + 4 + 4 * n_groups;
+  uint8_t* pad_group = reinterpret_cast<uint8_t*>(glist + n_groups);
+  // padding-group dedupe needs the token ids (gathered rows), 16-B aligned id rows
+  const bool dedupe = title_dedupe() && ids_a != nullptr &&
+                      (((uintptr_t)ids_a | (uintptr_t)(ids_b ? ids_b : ids_a)) % 16) == 0;
+  const GroupList gl{dedupe ? glist : nullptr, rcount + 1, rcount + 2};
   if (x6) {
     const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
     hipLaunchKernelGGL(pack_additive_b3_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
@@ -704,13 +807,24 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   }
   const int64_t blocks = n_groups < n_cu ? n_groups : n_cu;   // persistent: one workgroup per CU
   RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows};
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, n_groups,
-                     ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
+  if (dedupe) {
+    hipLaunchKernelGGL(classify_groups_kernel, dim3((unsigned)((n_groups + 255) / 256)), dim3(256), 0, s,
+                       rm, n_groups, glist, rcount + 1, rcount + 2, pad_group);
+    if (int32_t st = launch_status()) return st;
+  }
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, gl, ws,
+                     b_add, q_add, out, rl NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
   // the recheck pass: reads the count the main pass left; exits at once when 0
   const int64_t blocks_x = blocks < 64 ? blocks : 64;
-  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes, s, qkv, ldq, rm,
-                     n_groups, ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
+  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, gl,
+                     ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
+  if (int32_t st = launch_status()) return st;
+  if (dedupe) {
+    const int64_t nt4 = n_titles * (FD / 4);
+    hipLaunchKernelGGL(broadcast_padding_kernel, dim3((unsigned)((nt4 + 255) / 256)), dim3(256), 0, s,
+                       pad_group, rcount + 2, n_titles, out);
+  }
   return launch_status();
 }
 

@@ -185,6 +185,12 @@ bool fused_user_supported(int L, int D, int H, int Q);
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
                           hipStream_t s);
+// Process-wide switch (news_fused.hip): encode one all-padding title per
+// batch and broadcast its vector (nrms_set_title_dedupe; NRMS_DEDUPE=0 in the
+// environment turns it off).
+int title_dedupe();
+int set_title_dedupe(int on);
+
 // workspace of launch_fused_news: packed W_add, special rows, recheck list
 size_t fused_news_workspace_floats(int64_t n_titles);
 bool fused_news_supported(int L, int D, int H, int Q);

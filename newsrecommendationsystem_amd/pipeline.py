@@ -128,10 +128,13 @@ class ForwardPlan:
 
     # Algorithmic work per launch of each stage (SURVEY §8d conventions:
     # GEMMs 2·M·N·K; bytes = operands the stage must read + results it writes).
-    def work(self):
+    def work(self, titles_encoded=None):
+        """titles_encoded: titles the fused news tail actually encodes (with
+        padding-title dedupe: the non-padding titles + 1); default all."""
         B, C, Nc, L, D, V = self.B, self.C, self.N, self.L, self.D, self.V
         Q, H, dk = 200, 15, D // 15
         n_all, n_clk = B * (C + Nc), B * Nc
+        n_enc = n_all if titles_encoded is None else titles_encoded
         att_flop = lambda seqs, l: seqs * H * 2 * (2 * l * l * dk)
         qkv_m = V if self.folded else n_all * L
         return {
@@ -144,11 +147,11 @@ class ForwardPlan:
             "pool_news": dict(flop=2 * n_all * L * D, bytes=4 * (n_all * L * (D + 1) + n_all * D)),
             # fused tail: gathered q|k|v rows + ids in, news vectors out, W_add
             # (the context tile stays in LDS)
-            "news_fused": dict(flop=att_flop(n_all, L) + 2 * n_all * L * D * Q + 2 * n_all * L * D,
-                               bytes=n_all * L * (4 * 3 * D + (8 if self.folded else 0))
+            "news_fused": dict(flop=att_flop(n_enc, L) + 2 * n_enc * L * D * Q + 2 * n_enc * L * D,
+                               bytes=n_enc * L * (4 * 3 * D + (8 if self.folded else 0))
                                + 4 * (n_all * D + Q * D),
-                               split=dict(attention=att_flop(n_all, L), gemm=2 * n_all * L * D * Q,
-                                          pool=2 * n_all * L * D)),
+                               split=dict(attention=att_flop(n_enc, L), gemm=2 * n_enc * L * D * Q,
+                                          pool=2 * n_enc * L * D)),
             "qkv_user": dict(flop=2 * n_clk * D * 3 * D, bytes=4 * (n_clk * 4 * D + 3 * D * D)),
             "mhsa_user": dict(flop=att_flop(B, Nc), bytes=4 * n_clk * 4 * D),
             "addscore_user": dict(flop=2 * n_clk * D * Q, bytes=4 * (n_clk * (D + 1) + Q * D)),

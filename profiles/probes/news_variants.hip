@@ -20,6 +20,9 @@ namespace nrms {
 void set_last_hip_error(hipError_t) {}
 int g_arith = NRMS_GEMM_SPLIT_BF16X6;
 int gemm_arith() { return g_arith; }
+void ensure_dynamic_lds(const void* fn, int bytes) {
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
 }
 
 #define CK(x)                                                              \

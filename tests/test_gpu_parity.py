@@ -509,3 +509,48 @@ def test_config2_news_encoder_100k_titles(device, gemm_mode):
     pick = np.sort(W.randint(8, 501, (512,), 0, n))
     ref = O.news_encode(titles.numpy()[pick], sd, np.float64)
     assert O.normwise_rel_err(_np(folded)[pick], ref).max() < 1e-3
+
+
+@pytest.mark.parametrize("pad_frac", [0.0, 0.45, 1.0])
+def test_padding_title_dedupe_is_bitwise_identical(device, pad_frac, gemm_mode):
+    """nrms_set_title_dedupe: encoding one all-padding 4-title group and
+    copying its slot vectors to the other all-padding groups gives bitwise the
+    same logits and news vectors as encoding every title, with no, some and
+    only padding titles (clicked and candidate slots), through nrms_forward and
+    get_news_vector."""
+    from newsrecommendationsystem_amd import _native as N
+    V, B = 3000, 96
+    sd = W.nrms_state(61, V)
+    m = _module(sd, V, device, hip_proj_mode=N.NRMS_PROJ_FOLDED)
+    cand, clk, _ = W.impressions(61, 3, B, V)
+    rng = np.random.default_rng(61)
+    clk = clk.copy()
+    cand = cand.copy()
+    if pad_frac == 1.0:
+        clk[:] = 0
+        cand[:] = 0
+    elif pad_frac > 0:
+        clk[rng.random(clk.shape[:2]) < pad_frac] = 0
+        cand[rng.random(cand.shape[:2]) < 0.1] = 0
+    else:
+        clk[clk.sum(-1) == 0, 0] = 1          # no all-zero title anywhere
+    titles = torch.from_numpy(np.concatenate([clk.reshape(-1, 20), cand.reshape(-1, 20)]))
+    lib = N.load()
+    outs = {}
+    prev = lib.nrms_set_title_dedupe(1)
+    try:
+        for on in (1, 0):
+            lib.nrms_set_title_dedupe(on)
+            with torch.no_grad():
+                y = m.forward_ids(torch.from_numpy(cand), torch.from_numpy(clk))
+                v = m.get_news_vector({"title": titles})
+            outs[on] = (y.clone(), v.clone())
+    finally:
+        lib.nrms_set_title_dedupe(prev)
+    assert torch.equal(outs[1][0], outs[0][0])
+    assert torch.equal(outs[1][1], outs[0][1])
+    assert torch.isfinite(outs[1][0]).all()
+    pad = (titles == 0).all(dim=1)
+    if pad.any():   # one vector per slot; slots agree to fp32 rounding
+        vp = outs[1][1][pad.to(device)]
+        assert float((vp - vp[:1]).abs().max()) <= 1e-6 * float(vp.abs().max())
