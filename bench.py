@@ -248,7 +248,9 @@ def issue_floor_ms(stage, w, gemm):
     if stage != "news_fused":
         return None
     f = w["split"]
-    gemm_s = f["gemm"] * 6 / (PEAK_TFLOPS_BF16 * 1e12) if gemm == "x6" else f["gemm"] / (PEAK_TFLOPS_F32 * 1e12)
+    products = {"x6": 6, "f16x3": 3}.get(gemm)
+    gemm_s = (f["gemm"] * products / (PEAK_TFLOPS_BF16 * 1e12) if products
+              else f["gemm"] / (PEAK_TFLOPS_F32 * 1e12))
     rest_s = (f["attention"] + f["pool"]) / (PEAK_TFLOPS_F32 * 1e12)
     return (gemm_s + rest_s) * 1e3
 
@@ -277,8 +279,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend for the barrier / max-over-ranks timing (nccl = RCCL); "
                          "gloo lets several ranks share one GPU for a rehearsal")
-    ap.add_argument("--gemm", choices=["x6", "f32"], default="x6",
-                    help="GEMM arithmetic: split-bf16 x6 (fp32-accurate, default) or exact f32 MFMA")
+    ap.add_argument("--gemm", choices=["f16x3", "x6", "f32"], default="f16x3",
+                    help="GEMM arithmetic: split-f16 x3 additive GEMM + split-bf16 x6 projections "
+                         "(default), split-bf16 x6 everywhere, or exact f32 MFMA (all fp32-accurate)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -300,7 +303,8 @@ def main():
     from newsrecommendationsystem_amd import stream as S
     from newsrecommendationsystem_amd.pipeline import ForwardPlan
 
-    Nat.load().nrms_set_gemm_arith(Nat.NRMS_GEMM_SPLIT_BF16X6 if args.gemm == "x6" else Nat.NRMS_GEMM_F32)
+    Nat.load().nrms_set_gemm_arith({"f16x3": Nat.NRMS_GEMM_SPLIT_F16X3, "x6": Nat.NRMS_GEMM_SPLIT_BF16X6,
+                                    "f32": Nat.NRMS_GEMM_F32}[args.gemm])
     mode = {"folded": Nat.NRMS_PROJ_FOLDED, "direct": Nat.NRMS_PROJ_DIRECT, "auto": Nat.NRMS_PROJ_AUTO}[args.proj]
     model = build_model(device)
     B = args.batch
@@ -394,27 +398,35 @@ def main():
     roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 4), "traffic": load_traffic(dom),
                 "algorithmic_per_launch": {"flop": w["flop"], "bytes": w["bytes"]},
-                "peak_note": "fp32 MFMA/vector peak; the x6 GEMM issues 6 bf16 products per fp32 "
-                             "product, so see issue_floor for the instruction-level ceiling"}
+                "peak_note": "fp32 MFMA/vector peak; the split GEMMs issue 3 (f16x3) or 6 (x6) 16-bit "
+                             "products per fp32 product, so see issue_floor for the instruction-level "
+                             "ceiling"}
     if floor is not None:
         roofline["issue_floor"] = {
             "ms": round(floor, 4), "frac": round(floor / stage_ms[dom], 4),
-            "basis": ("additive GEMM x6 bf16 products at 2.5 PF dense + attention contractions "
-                      "and pooling at 157.3 TF" if args.gemm == "x6" else "all at 157.3 TF (f32 MFMA)"),
+            "basis": (f"additive GEMM {args.gemm} ({ {'x6': 6, 'f16x3': 3}.get(args.gemm)} 16-bit products "
+                      "per fp32 product) at 2.5 PF dense + attention contractions and pooling at 157.3 TF"
+                      if args.gemm != "f32" else "all at 157.3 TF (f32 MFMA)"),
             "flop_split": w["split"]}
     if sq is not None:
         roofline["sq_counters"] = sq
     workload = ("BASELINE cfg4: full NRMS forward over the whole user-sharded stream "
                 f"({idx.numel() if not dist else 'per-rank shards of'} impressions"
-                f"{'' if dist else ' on this GPU'}), every title encoded"
+                f"{'' if dist else ' on this GPU'}), every title's vector produced (all-padding "
+                "history groups encoded once per batch, see titles)"
                 if args.stream else
                 "BASELINE cfg3: full NRMS forward scoring (news+user encoder+click predictor), "
-                "every title encoded; batch = first B impressions of this rank's cfg4 user shard")
+                "every title's vector produced (all-padding history groups encoded once per batch, see "
+                "titles); batch = first B impressions of this rank's cfg4 user shard")
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "impressions/s", "n_gpus": world,
         "steps": steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
         "higher_is_better": True, "scaling": "strong" if args.stream else "weak", "vs_baseline": None,
-        "dtype": "fp32" if args.gemm == "f32" else "fp32 (GEMMs: exact 3-way bf16 split, 6 products, fp32 accumulate)",
+        "dtype": {"f32": "fp32",
+                  "x6": "fp32 (GEMMs: exact 3-way bf16 split, 6 products, fp32 accumulate)",
+                  "f16x3": "fp32 (additive GEMM: 2-plane fp16 split, 22-bit operands, 3 products, fp32 "
+                           "accumulate, out-of-fp16-range groups recomputed x6; projections: 3-way bf16 "
+                           "split, 6 products)"}[args.gemm],
         "data": "synthetic (MIND-shaped stream: counter-hash ids, random-init weights, N(0,1) embedding table)",
         "config": {"workload": workload, "global_batch": B * world,
                    "impressions_per_gpu": B, "candidates": C, "clicked": N_CLICKED,

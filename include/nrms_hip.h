@@ -78,17 +78,31 @@ typedef enum { NRMS_PROJ_AUTO = 0, NRMS_PROJ_DIRECT = 1, NRMS_PROJ_FOLDED = 2 } 
 
 /* Arithmetic of the matrix-core GEMMs (Q|K|V projections and the news
  * encoder's additive projection; attention contractions are always f32 MFMA).
- * SPLIT_BF16X6 (default): each fp32 operand is split exactly into three bf16
- * planes (hi + mid + lo, 8 significand bits each) and the six plane products
- * with i + j <= 2 are accumulated in fp32 on v_mfma_f32_16x16x32_bf16; every
- * bf16 product is exact and the dropped terms are below 2^-25 |a||b|, so the
- * result has fp32-GEMM accuracy (measured: normwise error vs fp64 at or below
- * the F32 mode's) at 6/16 of the f32-MFMA cycles. F32: v_mfma_f32_16x16x4_f32,
- * each product an exact fp32 FMA. Process-wide; the initial value comes from
- * the environment (NRMS_GEMM=f32 selects F32). Returns the previous mode, or
+ * SPLIT_BF16X6: each fp32 operand is split exactly into three bf16 planes
+ * (hi + mid + lo, 8 significand bits each) and the six plane products with
+ * i + j <= 2 are accumulated in fp32 on v_mfma_f32_16x16x32_bf16; every bf16
+ * product is exact and the dropped terms are below 2^-25 |a||b|, so the result
+ * has fp32-GEMM accuracy (measured: normwise error vs fp64 at or below the F32
+ * mode's) at 6/16 of the f32-MFMA cycles.
+ * SPLIT_F16X3 (default): the news encoder's additive projection splits each
+ * operand into two fp16 planes, a = hi + 2^-11 lo (22 significand bits), and
+ * accumulates hi·hi and hi·lo + lo·hi in two fp32 accumulators on
+ * v_mfma_f32_16x16x32_f16 (3 products instead of 6); the dropped terms are
+ * ~2^-22 |a||b|, normwise error vs fp64 still below a plain fp32 GEMM's. An
+ * operand outside fp16's range (|a| >= 65,520) turns its outputs into NaN,
+ * and those title groups are recomputed by the SPLIT_BF16X6 / reference-exp
+ * recheck pass, so results never depend on the range. The other GEMMs run
+ * SPLIT_BF16X6 in this mode.
+ * F32: v_mfma_f32_16x16x4_f32, each product an exact fp32 FMA.
+ * Process-wide; the initial value comes from the environment (NRMS_GEMM=f32
+ * selects F32, NRMS_GEMM=x6 SPLIT_BF16X6). Returns the previous mode, or
  * -NRMS_ERR_INVALID_ARG for an unknown mode. Not synchronised with launches
  * in flight: set it before enqueuing work. */
-typedef enum { NRMS_GEMM_SPLIT_BF16X6 = 0, NRMS_GEMM_F32 = 1 } nrms_gemm_arith_t;
+typedef enum {
+  NRMS_GEMM_SPLIT_BF16X6 = 0,
+  NRMS_GEMM_F32 = 1,
+  NRMS_GEMM_SPLIT_F16X3 = 2
+} nrms_gemm_arith_t;
 int32_t nrms_set_gemm_arith(int32_t mode);
 int32_t nrms_get_gemm_arith(void);
 

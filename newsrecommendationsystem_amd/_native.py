@@ -15,9 +15,10 @@ LIB_PATH = os.environ.get("NRMS_LIB_PATH") or os.path.join(_PKG, "libnrms_hip.so
 ABI_VERSION = 2
 
 NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
-NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32 = 0, 1
+NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32, NRMS_GEMM_SPLIT_F16X3 = 0, 1, 2
 NRMS_OK, NRMS_ERR_INVALID_ARG, NRMS_ERR_UNSUPPORTED, NRMS_ERR_WORKSPACE, NRMS_ERR_HIP = 0, 1, 2, 3, 4
-GEMM_ARITH_NAMES = {NRMS_GEMM_SPLIT_BF16X6: "split-bf16x6", NRMS_GEMM_F32: "f32"}
+GEMM_ARITH_NAMES = {NRMS_GEMM_SPLIT_BF16X6: "split-bf16x6", NRMS_GEMM_F32: "f32",
+                    NRMS_GEMM_SPLIT_F16X3: "split-f16x3"}
 
 _p = ctypes.c_void_p
 _i32 = ctypes.c_int32

@@ -17,7 +17,9 @@ void set_last_hip_error(hipError_t e) { g_last_hip = (int32_t)e; }
 
 static int initial_gemm_arith() {
   const char* e = getenv("NRMS_GEMM");
-  return (e && (e[0] == 'f' || e[0] == 'F')) ? NRMS_GEMM_F32 : NRMS_GEMM_SPLIT_BF16X6;
+  if (e && (e[0] == 'f' || e[0] == 'F')) return NRMS_GEMM_F32;
+  if (e && (e[0] == 'x' || e[0] == 'X')) return NRMS_GEMM_SPLIT_BF16X6;
+  return NRMS_GEMM_SPLIT_F16X3;
 }
 static std::atomic<int> g_gemm_arith{initial_gemm_arith()};
 int gemm_arith() { return g_gemm_arith.load(std::memory_order_relaxed); }
@@ -137,7 +139,8 @@ extern "C" {
 int32_t nrms_abi_version(void) { return NRMS_ABI_VERSION; }
 
 int32_t nrms_set_gemm_arith(int32_t mode) {
-  if (mode != NRMS_GEMM_SPLIT_BF16X6 && mode != NRMS_GEMM_F32) return -NRMS_ERR_INVALID_ARG;
+  if (mode != NRMS_GEMM_SPLIT_BF16X6 && mode != NRMS_GEMM_F32 && mode != NRMS_GEMM_SPLIT_F16X3)
+    return -NRMS_ERR_INVALID_ARG;
   return g_gemm_arith.exchange(mode);
 }
 

@@ -432,7 +432,7 @@ int32_t launch_gemm_store_rows(const float* X, int64_t n_rows_x, ARows ar, const
     return NRMS_ERR_UNSUPPORTED;
   for (int i = 0; i < w.nseg; ++i)
     if (((uintptr_t)w.w[i] % 16) != 0) return NRMS_ERR_UNSUPPORTED;
-  if (gemm_arith() == NRMS_GEMM_SPLIT_BF16X6) {
+  if (gemm_arith() != NRMS_GEMM_F32) {
     // 192-wide column tiles; a last partial tile of <= 160 columns runs the
     // TNW = 5 instantiation (N = 900: 4 x 192 + 132)
     const int nct = (N + 191) / 192;
@@ -466,7 +466,7 @@ int32_t launch_gemm_store_f32(const float* X, int64_t M, int K, const WeightRows
   if (M == 0) return NRMS_OK;
   // the training dX GEMMs: split-bf16 x6 like the forward projections unless
   // exact f32 MFMA is selected (NRMS_GEMM=f32)
-  if (gemm_arith() == NRMS_GEMM_SPLIT_BF16X6) return launch_gemm_store(X, M, nullptr, M, K, w, N, Y, ldy, s);
+  if (gemm_arith() != NRMS_GEMM_F32) return launch_gemm_store(X, M, nullptr, M, K, w, N, Y, ldy, s);
   if (K % 4 != 0 || ((uintptr_t)X % 16) != 0) return NRMS_ERR_UNSUPPORTED;
   for (int i = 0; i < w.nseg; ++i)
     if (((uintptr_t)w.w[i] % 16) != 0) return NRMS_ERR_UNSUPPORTED;

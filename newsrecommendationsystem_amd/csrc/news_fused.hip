@@ -87,6 +87,40 @@ static_assert((FROWS * XRB * 2) % 16 == 0 && (XRB * 2) % 16 == 0, "x6 row stride
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
+// Split-f16 x3 variant (F16X3, main pass only): the context and Wa are split
+// into two fp16 planes, a = hi + 2^-11 lo (hi = fp16(a), lo = fp16((a - hi)
+// 2^11): 11 + 11 significand bits; the scaled residual stays normal down to
+// |a| ~ 6e-5 and never overflows where hi does not). Wa also keeps a third
+// plane, hi' = 2^11 hi (exact), so the three products lo·hi, hi·lo, hi·hi'
+// all carry the factor 2^11 and sum in ONE fp32 accumulator on
+// v_mfma_f32_16x16x32_f16 (exact fp16 products): Y = 2^-11 acc. The dropped
+// lo·lo term and the operand residuals are ~2^-22 |a||b| — normwise error
+// below a plain fp32 GEMM's at half the x6 MFMA count.
+// fp16's range is the price. A context value at or beyond 65,520 becomes inf
+// in hi and -inf in lo, so lo·hi + hi·hi' is inf - inf = NaN in every output
+// column of its row; a weight with |hi'| past fp16 is packed as NaN. Either
+// way the row's score is NaN, and the score check in C routes the group to
+// the recheck pass (x6 + reference exp), as it does for NaN inputs.
+// Row stride 720 halves = 360 dwords (= 40 mod 64, 8 mod 32): the same bank
+// pattern as the x6 stride, conflict-free for the fragment reads and the
+// plane stores.
+constexpr int XRH = 2 * XKP + 80;
+constexpr int WAP2_FLOATS = XKS * FNT * 3 * 64 * 4;   // [ks][nt][plane hi' | lo | hi][lane][8 f16]
+constexpr size_t LDS_BYTES_H = (size_t)FROWS * XRH * 2 + (4 * FROWS + 2 * 2 * FROWS) * sizeof(float);
+static_assert(LDS_BYTES_H <= 160 * 1024 && (XRH / 2) % 64 == 40, "f16x3 row stride");
+constexpr float kLoScale = 2048.0f, kLoUnscale = 1.0f / 2048.0f;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 nrms_f16x2 __attribute__((ext_vector_type(2)));
+
+// fp16 split of two floats at once: packed hi words and scaled-residual words
+// (one v_cvt_pk_f16_f32 per plane, residual on v_pk_add / v_pk_mul).
+__device__ __forceinline__ void split2x2h(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+  const nrms_f16x2 h = __builtin_convertvector((nrms_f32x2){x0, x1}, nrms_f16x2);
+  const nrms_f32x2 r = ((nrms_f32x2){x0, x1} - __builtin_convertvector(h, nrms_f32x2)) * kLoScale;
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, nrms_f16x2));
+}
+
 __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
   hi = (__bf16)x;
   const float r = x - (float)hi;
@@ -124,6 +158,9 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
 
 // X6: WaP3[ks][nt][plane][lane][8] bf16 = plane of Wa[16 nt + (lane & 15)][32 ks + 8 (lane >> 4) + i]
 // (the B-operand fragments of v_mfma_f32_16x16x32_bf16), zero past Q or D.
+// F16: also the fp16 planes WaP2[ks][nt][plane][lane][8] (2^11 hi, the
+// 2^11-scaled residual, hi) after the special rows, for the F16X3 main pass.
+template <bool F16>
 __global__ __launch_bounds__(256) void pack_additive_b3_kernel(const float* __restrict__ Wa,
                                                                float* __restrict__ WaP,
                                                                int32_t* __restrict__ recheck_count) {
@@ -145,6 +182,15 @@ __global__ __launch_bounds__(256) void pack_additive_b3_kernel(const float* __re
   o[0] = hi;
   o[64 * 8] = mid;
   o[2 * 64 * 8] = lo;
+  if constexpr (F16) {
+    const _Float16 h = (_Float16)v;
+    _Float16* o2 = reinterpret_cast<_Float16*>(WaP + WAP_MAX + SPECIAL_FLOATS) +
+                   (((ks * FNT + nt) * 3) * 64 + lane) * 8 + i;
+    const float hs = (float)h * kLoScale;   // exact unless it overflows fp16: NaN then (-> recheck)
+    o2[0] = fabsf(hs) < 65504.f ? (_Float16)hs : (_Float16)qnan();
+    o2[64 * 8] = (_Float16)((v - (float)h) * kLoScale);
+    o2[2 * 64 * 8] = h;
+  }
 }
 
 
@@ -312,7 +358,8 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 }
 
 // MODE 0: f32 MFMA additive GEMM, fp32 context tile. MODE 1: split-bf16 x6,
-// context stored as bf16 planes.
+// context stored as bf16 planes. MODE 2: split-f16 x3 (main pass only; its
+// recheck pass runs MODE 1), context stored as fp16 planes.
 template <int MODE, bool EXACT>
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const float* __restrict__ qkv, int64_t ldq, RowMap rmap, GroupList gl,
@@ -321,10 +368,13 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     RecheckList rl NRMS_TIMING_PARAM) {
   using Off = QkvOffsets;
   constexpr bool X6 = MODE == 1;
+  constexpr bool H3 = MODE == 2;
+  static_assert(!(H3 && EXACT), "the F16X3 main pass is rechecked by the x6 kernel");
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* ctxL = lds;                                   // f32: [80][SC]
   __bf16* ctxB = reinterpret_cast<__bf16*>(lds);       // x6:  [80][XRB] = hi | mid | lo planes
-  float* part = X6 ? lds + FROWS * XRB / 2 : ctxL + FROWS * SC;   // [80][4] per-wave row partials
+  _Float16* ctxH = reinterpret_cast<_Float16*>(lds);   // f16x3: [80][XRH] = hi | lo planes
+  float* part = X6 ? lds + FROWS * XRB / 2 : (H3 ? lds + FROWS * XRH / 2 : ctxL + FROWS * SC);   // [80][4] per-wave row partials
   const float** rowptr = reinterpret_cast<const float**>(part + 4 * FROWS);   // [2][80]
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -339,6 +389,12 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #pragma unroll
         for (int c = 0; c < (XKP - FD) / 4; ++c)
           *reinterpret_cast<uint2*>(ctxB + tid * XRB + pl * XKP + FD + 4 * c) = make_uint2(0u, 0u);
+    } else if constexpr (H3) {
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl)
+#pragma unroll
+        for (int c = 0; c < (XKP - FD) / 4; ++c)
+          *reinterpret_cast<uint2*>(ctxH + tid * XRH + pl * XKP + FD + 4 * c) = make_uint2(0u, 0u);
     } else {
       *reinterpret_cast<float4*>(ctxL + tid * SC + FD) = make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -449,6 +505,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #endif
     NRMS_STAMP(0)
     floatx4 O[5][5];   // this wave's context rows, live until the pooling in C
+    uint64_t recheck = 0;   // lanes whose row needs the recheck pass (RecheckList)
 
     // ---------------- A: attention (4x4x1 MFMA, 16 (title, head) blocks) --------------
     {
@@ -463,7 +520,6 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       for (int j = 0; j < 5; ++j)
 #pragma unroll
         for (int i = 0; i < 5; ++i) S[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-      uint64_t recheck = 0;   // lanes whose row needs the reference's exp (RecheckList)
       // One query column i at a time (S^T, exp, ctx^T, split + store), so a
       // column's S registers die before the next column's are written: short
       // live ranges, no spills (all S^T first, then all ctx^T: 2 % slower;
@@ -511,7 +567,20 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       // stores into the next column's MFMAs and spills)
       auto o_store = [&](int i) {
         if (!hval) return;
-        if constexpr (X6) {
+        if constexpr (H3) {
+          _Float16* dst = ctxH + (FL * at + 4 * i + x) * XRH + FDK * h;
+#pragma unroll
+          for (int c = 0; c < FDK / 4; ++c) {
+            uint32_t hw[2], lw[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int d = 4 * c + 2 * e;
+              split2x2h(O[d % 5][i][d / 5], O[(d + 1) % 5][i][(d + 1) / 5], hw[e], lw[e]);
+            }
+            *reinterpret_cast<uint2*>(dst + 4 * c) = make_uint2(hw[0], hw[1]);
+            *reinterpret_cast<uint2*>(dst + XKP + 4 * c) = make_uint2(lw[0], lw[1]);
+          }
+        } else if constexpr (X6) {
           __bf16* dst = ctxB + (FL * at + 4 * i + x) * XRB + FDK * h;
 #pragma unroll
           for (int c = 0; c < FDK / 4; ++c) {
@@ -541,9 +610,6 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         s_exp(i);
         o_mfma(i);
         o_store(i);
-      }
-      if constexpr (!EXACT) {
-        if (recheck != 0 && lane == 0) rl.list[atomicAdd(rl.count, 1)] = (int32_t)tg;
       }
       store_row(next_row, nbuf);
     }
@@ -615,6 +681,62 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           case 2: mainloop(std::integral_constant<int, 2>{}); break;
           default: mainloop(std::integral_constant<int, 3>{}); break;
         }
+      } else if constexpr (H3) {
+        // products lo·hi, hi·lo, hi·hi' (each 2^11 x the true product) into acc
+        const _Float16* Ah = ctxH + lm * XRH + 8 * kq;
+        const f16x8* Bq = reinterpret_cast<const f16x8*>(WaP + WAP_MAX + SPECIAL_FLOATS) + lane;
+        // B plane pb: 0 = hi', 1 = lo, 2 = hi; loaded in consumption order
+        auto load_b = [&](int ks, f16x8 (&dst)[4][3]) {
+#pragma unroll
+          for (int pl = 2; pl >= 0; --pl)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const int nt = j < 3 ? 3 * w + j : 12;
+              dst[j][pl] = Bq[((ks * FNT + nt) * 3 + pl) * 64];
+            }
+        };
+        auto kstep = [&](int ks, const f16x8 (&bb)[4][3], auto wc) {
+          constexpr int W = decltype(wc)::value;
+          constexpr bool EXTRA = W == 0;
+          f16x8 a[FMT][2];
+#pragma unroll
+          for (int pl = 1; pl >= 0; --pl)
+#pragma unroll
+            for (int mt = 0; mt < FMT; ++mt)
+              a[mt][pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * mt * XRH + pl * XKP + 32 * ks);
+          const f16x8 (&ax)[2] = a[W];
+#define NRMS_H3STEP(PA, PB)                                                                            \
+  _Pragma("unroll") for (int mt = 0; mt < FMT; ++mt)                                                   \
+  _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                        \
+      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);  \
+  accX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ax[PA], bb[3][PB], accX, 0, 0, 0);                     \
+  if constexpr (EXTRA) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[FMT - 1][PA], bb[3][PB], accX2, 0, 0, 0);
+          NRMS_H3STEP(1, 2) NRMS_H3STEP(0, 1) NRMS_H3STEP(0, 0)
+#undef NRMS_H3STEP
+        };
+        auto mainloop = [&](auto extra) {
+          f16x8 b0[4][3], b1[4][3];
+          load_b(0, b0);
+#pragma unroll 1   // (unrolled, the 3-product k-steps spill ~700 registers)
+          for (int ks = 0; ks < XKS; ks += 2) {
+            load_b(ks + 1, b1);
+            kstep(ks, b0, extra);
+            if (ks + 2 < XKS) load_b(ks + 2, b0);
+            kstep(ks + 1, b1, extra);
+          }
+        };
+        switch (w) {
+          case 0: mainloop(std::integral_constant<int, 0>{}); break;
+          case 1: mainloop(std::integral_constant<int, 1>{}); break;
+          case 2: mainloop(std::integral_constant<int, 2>{}); break;
+          default: mainloop(std::integral_constant<int, 3>{}); break;
+        }
+#pragma unroll
+        for (int mt = 0; mt < FMT; ++mt)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[mt][j] *= kLoUnscale;
+        accX *= kLoUnscale;
+        accX2 *= kLoUnscale;
       } else {
       float4 bb[4], bn[4];
 #pragma unroll
@@ -683,6 +805,16 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         const float4 pv = *reinterpret_cast<const float4*>(part + 4 * (FL * at + 4 * i + x));
         sc[i] = ((pv.x + pv.y) + pv.z) + pv.w;
       }
+      if constexpr (H3) {
+        // a NaN score: an operand beyond fp16's range (or NaN inputs) -> recheck pass
+        bool bad = false;
+#pragma unroll
+        for (int i = 0; i < 5; ++i) bad |= sc[i] != sc[i];
+        recheck |= __builtin_amdgcn_ballot_w64(bad);
+      }
+      if constexpr (!EXACT) {
+        if (recheck != 0 && lane == 0) rl.list[atomicAdd(rl.count, 1)] = (int32_t)tg;
+      }
       float mx = sc[0];
 #pragma unroll
       for (int i = 1; i < 5; ++i) mx = nan_max(mx, sc[i]);
@@ -741,7 +873,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 
 // packed W_add + special rows, then int32 [recheck count, group-list count,
 // rep, 0], the recheck list (4 per group), the group list, pad_group bytes
-static size_t fused_news_list_offset() { return (size_t)WAP_MAX + SPECIAL_FLOATS; }
+static size_t fused_news_list_offset() { return (size_t)WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS; }
 size_t fused_news_workspace_floats(int64_t n_titles) {
   const int64_t n_groups = (n_titles + FT - 1) / FT;
   return fused_news_list_offset() + 4 + 4 * (size_t)n_groups + (size_t)n_groups +
@@ -775,12 +907,16 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   if (ldq < ROW || ldq % 4) return NRMS_ERR_UNSUPPORTED;   // float4 q / k slices
   const int64_t n_groups = (n_titles + FT - 1) / FT;
   if (4 * n_groups > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
-  const bool x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6;
-  auto kern = x6 ? &fused_news_kernel<1, false> : &fused_news_kernel<0, false>;
+  // F16X3: f16x3 main pass, x6 recheck pass
+  const int arith = gemm_arith();
+  const bool h3 = arith == NRMS_GEMM_SPLIT_F16X3;
+  const bool x6 = arith != NRMS_GEMM_F32;
+  auto kern = h3 ? &fused_news_kernel<2, false> : (x6 ? &fused_news_kernel<1, false> : &fused_news_kernel<0, false>);
   auto kern_exact = x6 ? &fused_news_kernel<1, true> : &fused_news_kernel<0, true>;
-  const size_t lds_bytes = x6 ? LDS_BYTES_X6 : LDS_BYTES;
+  const size_t lds_bytes = h3 ? LDS_BYTES_H : (x6 ? LDS_BYTES_X6 : LDS_BYTES);
+  const size_t lds_bytes_exact = x6 ? LDS_BYTES_X6 : LDS_BYTES;
   ensure_dynamic_lds(reinterpret_cast<const void*>(kern), (int)lds_bytes);
-  ensure_dynamic_lds(reinterpret_cast<const void*>(kern_exact), (int)lds_bytes);
+  ensure_dynamic_lds(reinterpret_cast<const void*>(kern_exact), (int)lds_bytes_exact);
   int32_t* rcount = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
   const RecheckList rl{rcount, rcount + 4};
   int32_t* glist = rcount + 4 + 4 * n_groups;
@@ -791,8 +927,12 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   const GroupList gl{dedupe ? glist : nullptr, rcount + 1, rcount + 2};
   if (x6) {
     const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
-    hipLaunchKernelGGL(pack_additive_b3_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
-                       rcount);
+    if (h3)
+      hipLaunchKernelGGL(pack_additive_b3_kernel<true>, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
+                         rcount);
+    else
+      hipLaunchKernelGGL(pack_additive_b3_kernel<false>, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
+                         rcount);
   } else {
     const int npk = WAP_FLOATS + SPECIAL_FLOATS;
     hipLaunchKernelGGL(pack_additive_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
@@ -817,7 +957,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   if (int32_t st = launch_status()) return st;
   // the recheck pass: reads the count the main pass left; exits at once when 0
   const int64_t blocks_x = blocks < 64 ? blocks : 64;
-  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, gl,
+  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes_exact, s, qkv, ldq, rm, gl,
                      ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
   if (dedupe) {

@@ -584,7 +584,7 @@ int32_t launch_gemm_tn(const float* dY, int64_t R, int N, const float* X, int K,
   const int64_t zs = (R + TN_ROWS - 1) / TN_ROWS;
   if (zs > 65535) return NRMS_ERR_UNSUPPORTED;
   dim3 grid((N + TN_TILE - 1) / TN_TILE, (K + TN_TILE - 1) / TN_TILE, (unsigned)zs);
-  const bool x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6 && N % 4 == 0 && K % 4 == 0 &&
+  const bool x6 = gemm_arith() != NRMS_GEMM_F32 && N % 4 == 0 && K % 4 == 0 &&
                   ((uintptr_t)dY | (uintptr_t)X) % 16 == 0;
   if (x6)
     hipLaunchKernelGGL(gemm_tn_x6_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, dW, db);

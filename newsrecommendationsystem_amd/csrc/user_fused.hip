@@ -405,7 +405,7 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16 || ldq < 3 * UD || ldq % 4)
     return NRMS_ERR_UNSUPPORTED;
-  const int x6 = gemm_arith() == NRMS_GEMM_SPLIT_BF16X6 ? 1 : 0;
+  const int x6 = gemm_arith() != NRMS_GEMM_F32 ? 1 : 0;
   const int npk = x6 ? UKS * UNT * 64 * 8 : UWAP1;
   hipLaunchKernelGGL(pack_user_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap, x6);
   if (int32_t st = launch_status()) return st;

@@ -47,11 +47,13 @@ def device():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=["x6", "f32"])
+@pytest.fixture(params=["f16x3", "x6", "f32"])
 def gemm_mode(request):
-    """Run a GPU test under both GEMM arithmetics (include/nrms_hip.h,
-    nrms_set_gemm_arith): split-bf16 x6 (default) and exact f32 MFMA."""
+    """Run a GPU test under every GEMM arithmetic (include/nrms_hip.h,
+    nrms_set_gemm_arith): split-f16 x3 (default), split-bf16 x6 and exact f32
+    MFMA."""
     from newsrecommendationsystem_amd import _native as N
-    mode = N.NRMS_GEMM_SPLIT_BF16X6 if request.param == "x6" else N.NRMS_GEMM_F32
+    mode = {"f16x3": N.NRMS_GEMM_SPLIT_F16X3, "x6": N.NRMS_GEMM_SPLIT_BF16X6,
+            "f32": N.NRMS_GEMM_F32}[request.param]
     with N.gemm_arith(mode):
         yield request.param

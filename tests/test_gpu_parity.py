@@ -399,10 +399,10 @@ def test_plan_matches_forward(device, fused, mode, gemm_mode):
     assert np.abs(_np(y) - O.forward(cand, clk, sd, np.float64)).max() <= TOL * np.abs(_np(y)).max()
 
 
-def test_split_bf16x6_accuracy_matches_f32(device):
-    """The split-bf16 x6 GEMMs are as accurate as the exact-f32 MFMA GEMMs:
-    against the fp64 oracle, the x6 forward's error is within 2x the f32
-    forward's (both ~1e-7 normwise), on the full vocabulary."""
+def test_split_gemm_accuracy_matches_f32(device):
+    """The split GEMMs are as accurate as the exact-f32 MFMA GEMMs: against
+    the fp64 oracle, the x6 and f16x3 forwards' errors are within 2x the f32
+    forward's (all ~1e-7 normwise), on the full vocabulary."""
     from newsrecommendationsystem_amd import _native as N
     V = 70976
     sd = W.nrms_state(17, V)
@@ -412,15 +412,90 @@ def test_split_bf16x6_accuracy_matches_f32(device):
     news_ids = W.titles(17, 78, 64, V, min_len=1)
     nref = O.news_encode(news_ids, sd, np.float64)
     errs = {}
-    for mode in (N.NRMS_GEMM_SPLIT_BF16X6, N.NRMS_GEMM_F32):
+    for mode in (N.NRMS_GEMM_SPLIT_BF16X6, N.NRMS_GEMM_F32, N.NRMS_GEMM_SPLIT_F16X3):
         with N.gemm_arith(mode), torch.no_grad():
             y = _np(m.forward_ids(torch.from_numpy(cand), torch.from_numpy(clk)))
             nv = _np(m.get_news_vector({"title": torch.from_numpy(news_ids)}))
         errs[mode] = (O.normwise_rel_err(y.reshape(1, -1), ref.reshape(1, -1)).max(),
                       O.normwise_rel_err(nv, nref).max())
-    x6, f32 = errs[N.NRMS_GEMM_SPLIT_BF16X6], errs[N.NRMS_GEMM_F32]
-    assert x6[0] < 1e-5 and x6[1] < 1e-5, errs
-    assert x6[0] <= 2 * f32[0] + 1e-7 and x6[1] <= 2 * f32[1] + 1e-7, errs
+    f32 = errs[N.NRMS_GEMM_F32]
+    for mode in (N.NRMS_GEMM_SPLIT_BF16X6, N.NRMS_GEMM_SPLIT_F16X3):
+        e = errs[mode]
+        assert e[0] < 1e-5 and e[1] < 1e-5, errs
+        assert e[0] <= 2 * f32[0] + 1e-7 and e[1] <= 2 * f32[1] + 1e-7, errs
+
+
+def _attention_pool(qkv, ldq, ids, w, device):
+    """nrms_news_attention_pool over a caller-made q|k|v table (one id array)."""
+    from newsrecommendationsystem_amd import _native as N
+    n = ids.shape[0]
+    out = torch.empty(n, 300, device=device)
+    nb = N.load().nrms_news_attention_pool_workspace_size(n, 20, 300)
+    ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    N.call("nrms_news_attention_pool", N.ptr(qkv), ldq, qkv.shape[0], N.ptr(ids), n, None, n, 20,
+           ctypes.byref(w), N.ptr(out), N.ptr(ws), nb, N.stream_handle(device))
+    return out
+
+
+def test_f16x3_out_of_range_context_takes_recheck(device):
+    """F16X3 range guard: value rows far beyond fp16's range (|v| ~ 1e6 on
+    every 7th vocabulary id) make the context of any title attending to them
+    overflow fp16, which the main pass turns into NaN scores; those title
+    groups must come out of the recheck pass (x6 GEMM, reference exp) finite
+    and within fp32 rounding of the SPLIT_BF16X6 result, like every other
+    title. (Not bitwise: the x6 main pass takes the fast exp; and the 1e6
+    dynamic range of the context inflates fp32 rounding differences, hence
+    1e-4 here.)"""
+    from newsrecommendationsystem_amd import _native as N
+    V, n = 700, 1001
+    sd = W.nrms_state(71, V)
+    m = _module(sd, V, device, hip_cache_folded_table=False)
+    g = torch.Generator().manual_seed(71)
+    qkv = torch.zeros(V, 928)
+    qkv[:, :600] = 0.3 * torch.randn(V, 600, generator=g)
+    qkv[:, 600:900] = torch.randn(V, 300, generator=g)
+    big = torch.arange(V) % 7 == 3
+    qkv[big, 600:900] *= 1e6
+    qkv = qkv.to(device)
+    ids = torch.from_numpy(W.titles(71, 72, n, V, min_len=1)).to(device)
+    w, keep = m.news_encoder.weights()
+    outs = {}
+    for mode in (N.NRMS_GEMM_SPLIT_F16X3, N.NRMS_GEMM_SPLIT_BF16X6):
+        with N.gemm_arith(mode):
+            outs[mode] = _attention_pool(qkv, 928, ids, w, device)
+    h3, x6 = outs[N.NRMS_GEMM_SPLIT_F16X3], outs[N.NRMS_GEMM_SPLIT_BF16X6]
+    assert torch.isfinite(x6).all()
+    hit = big.to(device)[ids].any(dim=1)                       # titles attending to a big row
+    grp = torch.nn.functional.pad(hit, (0, (-n) % 4)).view(-1, 4).any(dim=1)
+    in_grp = grp.repeat_interleave(4)[:n]
+    assert 0 < int(in_grp.sum()) < n
+    assert torch.isfinite(h3).all()
+    rel = ((h3 - x6).norm(dim=1) / x6.norm(dim=1)).max()
+    assert rel < 1e-4, float(rel)
+
+
+def test_f16x3_out_of_range_weight_takes_recheck(device):
+    """A W_add entry whose 2^11-scaled fp16 plane overflows (|w| >= 32) is
+    packed as NaN: every group is recomputed by the recheck pass (x6 GEMM,
+    reference exp), finite and within fp32 rounding of SPLIT_BF16X6 and the
+    fp64 oracle."""
+    from newsrecommendationsystem_amd import _native as N
+    V, n = 500, 203
+    sd = dict(W.nrms_state(73, V))
+    key = "news_encoder.additive_attention.linear.weight"
+    sd[key] = sd[key].copy()
+    sd[key][5, 17] = 40.0
+    m = _module(sd, V, device, hip_cache_folded_table=False)
+    titles = torch.from_numpy(W.titles(73, 74, n, V, min_len=1))
+    outs = {}
+    for mode in (N.NRMS_GEMM_SPLIT_F16X3, N.NRMS_GEMM_SPLIT_BF16X6):
+        with N.gemm_arith(mode), torch.no_grad():
+            outs[mode] = m.get_news_vector({"title": titles})
+    h3, x6 = outs[N.NRMS_GEMM_SPLIT_F16X3], outs[N.NRMS_GEMM_SPLIT_BF16X6]
+    assert torch.isfinite(x6).all() and torch.isfinite(h3).all()
+    assert ((h3 - x6).norm(dim=1) / x6.norm(dim=1)).max() < 1e-5
+    ref = O.news_encode(titles.numpy(), sd, np.float64)
+    assert O.normwise_rel_err(_np(outs[N.NRMS_GEMM_SPLIT_F16X3]), ref).max() < TOL
 
 
 @pytest.mark.parametrize("B,n_clk", [(3, 1), (5, 17), (257, 50), (4, 64)])

@@ -58,12 +58,17 @@ def test_exports_every_declared_symbol():
 
 
 def test_gemm_arith_setting_without_gpu():
-    """Process-wide GEMM arithmetic: default split-bf16x6 (unless NRMS_GEMM=f32),
-    settable, unknown modes rejected without changing the setting."""
+    """Process-wide GEMM arithmetic: default split-f16x3 (NRMS_GEMM=f32 / x6
+    select the others), settable, unknown modes rejected without changing the
+    setting."""
     from newsrecommendationsystem_amd import _native as N
     lib = N.load()
     start = lib.nrms_get_gemm_arith()
-    assert start in (N.NRMS_GEMM_SPLIT_BF16X6, N.NRMS_GEMM_F32)
+    assert start in (N.NRMS_GEMM_SPLIT_BF16X6, N.NRMS_GEMM_F32, N.NRMS_GEMM_SPLIT_F16X3)
+    if "NRMS_GEMM" not in os.environ:
+        assert start == N.NRMS_GEMM_SPLIT_F16X3
+    with N.gemm_arith(N.NRMS_GEMM_SPLIT_BF16X6):
+        assert lib.nrms_get_gemm_arith() == N.NRMS_GEMM_SPLIT_BF16X6
     with N.gemm_arith(N.NRMS_GEMM_F32):
         assert lib.nrms_get_gemm_arith() == N.NRMS_GEMM_F32
         assert lib.nrms_set_gemm_arith(7) < 0
