@@ -108,18 +108,8 @@ constexpr int XRH = 2 * XKP + 80;
 constexpr int WAP2_FLOATS = XKS * FNT * 3 * 64 * 4;   // [ks][nt][plane hi' | lo | hi][lane][8 f16]
 constexpr size_t LDS_BYTES_H = (size_t)FROWS * XRH * 2 + (4 * FROWS + 2 * 2 * FROWS) * sizeof(float);
 static_assert(LDS_BYTES_H <= 160 * 1024 && (XRH / 2) % 64 == 40, "f16x3 row stride");
-constexpr float kLoScale = 2048.0f, kLoUnscale = 1.0f / 2048.0f;
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 nrms_f16x2 __attribute__((ext_vector_type(2)));
-
-// fp16 split of two floats at once: packed hi words and scaled-residual words
-// (one v_cvt_pk_f16_f32 per plane, residual on v_pk_add / v_pk_mul).
-__device__ __forceinline__ void split2x2h(float x0, float x1, uint32_t& hi, uint32_t& lo) {
-  const nrms_f16x2 h = __builtin_convertvector((nrms_f32x2){x0, x1}, nrms_f16x2);
-  const nrms_f32x2 r = ((nrms_f32x2){x0, x1} - __builtin_convertvector(h, nrms_f32x2)) * kLoScale;
-  hi = __builtin_bit_cast(uint32_t, h);
-  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, nrms_f16x2));
-}
+constexpr float kLoScale = kF16LoScale, kLoUnscale = kF16LoUnscale;
+typedef nrms_f16x8 f16x8;
 
 __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
   hi = (__bf16)x;

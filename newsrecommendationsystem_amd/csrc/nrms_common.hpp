@@ -86,6 +86,29 @@ __device__ __forceinline__ void split3x2(float x0, float x1, uint32_t& hi, uint3
   lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((nrms_f32x2){s0, s1}, nrms_bf16x2));
 }
 
+// Split-f16 x3 operands (NRMS_GEMM_SPLIT_F16X3): x = hi + 2^-11 lo with
+// hi = fp16(x), lo = fp16((x - hi) 2^11) — 11 + 11 significand bits, relative
+// error ~2^-22 for |x| >= ~1.2e-4 and at most ~1.5e-11 absolute below it. The
+// residual scaled by 2^11 never overflows where hi does not; an x at or past
+// 65,520 gives hi = inf, lo = -inf, and every product sum it enters becomes
+// NaN. The weight side also keeps hi' = 2^11 hi (NaN where that overflows,
+// |w| >= 32), so lo·hi + hi·lo + hi·hi' = 2^11 x·w in one accumulator.
+// Used for the additive projections only: their outputs feed tanh and a
+// max-subtracted softmax, so ulp-level operand rounding has no boundary
+// effects there; the Q|K|V projections stay x6, whose exact operand split
+// keeps single-term products (and so the raw-exp overflow boundary of the
+// attention scores) bit-exact with the reference.
+constexpr float kF16LoScale = 2048.0f, kF16LoUnscale = 1.0f / 2048.0f;
+typedef _Float16 nrms_f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 nrms_f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 nrms_f16x8 __attribute__((ext_vector_type(8)));
+// packed [x0 | x1 << 16] words of hi and lo (one v_cvt_pk_f16_f32 per plane)
+__device__ __forceinline__ void split2x2h(float x0, float x1, uint32_t& hi, uint32_t& lo) {
+  const nrms_f16x2 h = __builtin_convertvector((nrms_f32x2){x0, x1}, nrms_f16x2);
+  const nrms_f32x2 r = ((nrms_f32x2){x0, x1} - __builtin_convertvector(h, nrms_f32x2)) * kF16LoScale;
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, nrms_f16x2));
+}
 // Bijective XCD-aware block remap (cdna_hip_programming.md §5, "XCD swizzle
 // must be bijective"): blocks dealt round-robin over 8 XCDs get contiguous
 // logical ids per XCD, so tiles that share operands share an L2.
