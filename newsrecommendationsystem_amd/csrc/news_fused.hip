@@ -617,16 +617,20 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       if constexpr (X6) {
         // A fragments (16x16x32): lane holds A[row lm][32 ks + 8 kq .. + 7] of each plane
         const __bf16* Ab = ctxB + lm * XRB + 8 * kq;
-        const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
+        // B fragments through a buffer resource (as the F16X3 path below)
+        const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(WaP), 0, WAP3_FLOATS * 4, 0x00020000);
+        int bvoff[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
         // plane-major: the hi planes (first product's B) arrive first
         auto load_b = [&](int ks, bf16x8 (&dst)[4][3]) {
 #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int nt = j < 3 ? 3 * w + j : 12;
-              dst[j][pl] = Bq[((ks * FNT + nt) * 3 + pl) * 64];
-            }
+            for (int j = 0; j < 4; ++j)
+              dst[j][pl] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                  brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
         };
         // one 32-deep k-step; EXTRA: wave 0 also owns (M-tile 4, N-tile 12)
         // the wave index is a template constant (the X tile's A rows = M-tile
@@ -657,11 +661,14 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         auto mainloop = [&](auto extra) {
           bf16x8 b0[4][3], b1[4][3];
           load_b(0, b0);
+#pragma unroll
           for (int ks = 0; ks < XKS; ks += 2) {
             load_b(ks + 1, b1);
             kstep(ks, b0, extra);
+            __builtin_amdgcn_sched_barrier(0);
             if (ks + 2 < XKS) load_b(ks + 2, b0);
             kstep(ks + 1, b1, extra);
+            __builtin_amdgcn_sched_barrier(0);
           }
         };
         static_assert(XKS % 2 == 0, "k-steps in pairs");
@@ -674,16 +681,21 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       } else if constexpr (H3) {
         // products lo·hi, hi·lo, hi·hi' (each 2^11 x the true product) into acc
         const _Float16* Ah = ctxH + lm * XRH + 8 * kq;
-        const f16x8* Bq = reinterpret_cast<const f16x8*>(WaP + WAP_MAX + SPECIAL_FLOATS) + lane;
+        // B fragments through a buffer resource: one VGPR offset (the lane), the
+        // fragment offset in an SGPR (no per-load address registers when unrolled)
+        const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+            const_cast<float*>(WaP + WAP_MAX + SPECIAL_FLOATS), 0, WAP2_FLOATS * 4, 0x00020000);
+        int bvoff[4];   // lane + N-tile in the VGPR offset; k-step in soffset; plane immediate
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
         // B plane pb: 0 = hi', 1 = lo, 2 = hi; loaded in consumption order
         auto load_b = [&](int ks, f16x8 (&dst)[4][3]) {
 #pragma unroll
           for (int pl = 2; pl >= 0; --pl)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-              const int nt = j < 3 ? 3 * w + j : 12;
-              dst[j][pl] = Bq[((ks * FNT + nt) * 3 + pl) * 64];
-            }
+            for (int j = 0; j < 4; ++j)
+              dst[j][pl] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                  brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
         };
         auto kstep = [&](int ks, const f16x8 (&bb)[4][3], auto wc) {
           constexpr int W = decltype(wc)::value;
@@ -707,12 +719,18 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         auto mainloop = [&](auto extra) {
           f16x8 b0[4][3], b1[4][3];
           load_b(0, b0);
-#pragma unroll 1   // (unrolled, the 3-product k-steps spill ~700 registers)
+          // fully unrolled, each k-step's loads and MFMAs fenced in place
+          // (without the fences the scheduler hoists every load: 1,100 spills);
+          // a rolled loop permuted the accumulators at its back-edge (~170
+          // AGPR moves per iteration): 1.41 -> 1.33 ms
+#pragma unroll
           for (int ks = 0; ks < XKS; ks += 2) {
             load_b(ks + 1, b1);
             kstep(ks, b0, extra);
+            __builtin_amdgcn_sched_barrier(0);
             if (ks + 2 < XKS) load_b(ks + 2, b0);
             kstep(ks + 1, b1, extra);
+            __builtin_amdgcn_sched_barrier(0);
           }
         };
         switch (w) {

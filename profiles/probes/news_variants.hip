@@ -1,5 +1,5 @@
-// Fused news kernel, both additive-GEMM variants (split-bf16 x6 and exact f32
-// MFMA) on the bench shape (56,320 titles, folded q|k|v table of V = 70,976
+// Fused news kernel, the three additive-GEMM variants (split-f16 x3,
+// split-bf16 x6 and exact f32 MFMA) on the bench shape (56,320 titles, folded q|k|v table of V = 70,976
 // rows): wall time per launch (HIP events), output agreement between the
 // variants, and the per-phase shader-cycle breakdown (s_memtime stamps
 // compiled in with NRMS_FUSED_TIMING; a diagnostic build, the stamps cost time).
@@ -49,7 +49,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < h_ids.size(); ++i) h_ids[i] = 1 + (int64_t)(rnd() * id_range);
   // a few padding tokens / an all-padding title, as the synthetic generator has
   for (int t = 0; t < 20; ++t) h_ids[7 * 20 + t] = 0;
-  float *qkv, *wa, *b, *q, *wap, *out0, *out1;
+  float *qkv, *wa, *b, *q, *wap, *out0, *out1, *out2;
   int64_t* ids;
   unsigned long long* dbg;
   CK(hipMalloc(&qkv, h_qkv.size() * 4));
@@ -59,6 +59,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&wap, nrms::fused_news_workspace_floats(n_titles) * 4));
   CK(hipMalloc(&out0, (size_t)n_titles * 300 * 4));
   CK(hipMalloc(&out1, (size_t)n_titles * 300 * 4));
+  CK(hipMalloc(&out2, (size_t)n_titles * 300 * 4));
   CK(hipMalloc(&ids, h_ids.size() * 8));
   CK(hipMalloc(&dbg, 256 * 8 * 8 * 8));
   CK(hipMemcpy(qkv, h_qkv.data(), h_qkv.size() * 4, hipMemcpyHostToDevice));
@@ -72,11 +73,12 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  const char* vname[2] = {"exact f32 MFMA", "split-bf16 x6"};
-  const int nwaves[2] = {4, 4};
-  float* outs[2] = {out0, out1};
-  for (int var = 1; var >= 0; --var) {
-    nrms::g_arith = var ? NRMS_GEMM_SPLIT_BF16X6 : NRMS_GEMM_F32;
+  const char* vname[3] = {"exact f32 MFMA", "split-bf16 x6", "split-f16 x3"};
+  const int nwaves[3] = {4, 4, 4};
+  const int arith[3] = {NRMS_GEMM_F32, NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_SPLIT_F16X3};
+  float* outs[3] = {out0, out1, out2};
+  for (int var = 2; var >= 0; --var) {
+    nrms::g_arith = arith[var];
     float* out = outs[var];
     for (int it = 0; it < 2; ++it)
       if (nrms::launch_fused_news(qkv, 900, V, ids, n_titles, nullptr, n_titles, wa, b, q, wap, out, 0)) return 2;
@@ -114,7 +116,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(c.data(), out0, c.size() * 4, hipMemcpyDeviceToHost));
   double worst_all = 0;
   size_t nan_all = 0;
-  for (int var = 1; var <= 1; ++var) {
+  for (int var = 1; var <= 2; ++var) {
     CK(hipMemcpy(a.data(), outs[var], a.size() * 4, hipMemcpyDeviceToHost));
     double worst = 0, num = 0, den = 0;
     size_t nan_mismatch = 0;
