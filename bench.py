@@ -255,10 +255,14 @@ def issue_floor_ms(stage, w, gemm):
     return (gemm_s + rest_s) * 1e3
 
 
-def run_plan_steps(plan, batches, steps, events=None):
+def n_all_titles(B):
+    return B * (C + N_CLICKED)
+
+
+def run_steps(fwd, batches, steps, events=None):
     for k in range(steps):
         cand, clk = batches[k % len(batches)]
-        plan.run(cand, clk, events[k] if events else None)
+        fwd.run(cand, clk, events[k] if events else None)
 
 
 def main():
@@ -301,7 +305,7 @@ def main():
 
     from newsrecommendationsystem_amd import _native as Nat
     from newsrecommendationsystem_amd import stream as S
-    from newsrecommendationsystem_amd.pipeline import ForwardPlan
+    from newsrecommendationsystem_amd.pipeline import ForwardPlan, TimedForward
 
     Nat.load().nrms_set_gemm_arith({"f16x3": Nat.NRMS_GEMM_SPLIT_F16X3, "x6": Nat.NRMS_GEMM_SPLIT_BF16X6,
                                     "f32": Nat.NRMS_GEMM_F32}[args.gemm])
@@ -318,32 +322,43 @@ def main():
         batches = [S.batch(0, idx, V_WORDS)]
     full = [b for b in batches if b[0].shape[0] == B]
     tail = [b for b in batches if b[0].shape[0] != B]
+    # the timed step is the product path itself (nrms_forward, stage events
+    # inside the library); ForwardPlan (the stage ABI, one call per stage)
+    # gives the per-stage algorithmic work and the --unfused stage kernels
     plan = ForwardPlan(model, B, C, N_CLICKED, L, proj_mode=mode, fused=not args.unfused)
-    tail_plan = (ForwardPlan(model, tail[0][0].shape[0], C, N_CLICKED, L, proj_mode=mode,
-                             fused=not args.unfused) if tail else None)
-    n_st = len(plan.stages)
+    fwd = plan if args.unfused else TimedForward(model, B, C, N_CLICKED, L, proj_mode=mode)
+    tail_fwd = None
+    if tail:
+        Bt = tail[0][0].shape[0]
+        tail_fwd = (ForwardPlan(model, Bt, C, N_CLICKED, L, proj_mode=mode, fused=False) if args.unfused
+                    else TimedForward(model, Bt, C, N_CLICKED, L, proj_mode=mode))
+    stages = fwd.stages
+    n_st = len(stages)
     steps = 50 if args.steps is None else args.steps
     if args.stream:
         steps = len(full) if not args.steps or args.steps > len(full) else args.steps
     cand, clk = full[0]
 
     with torch.no_grad():
-        run_plan_steps(plan, full, args.warmup)
-        if tail_plan is not None:
-            tail_plan.run(*tail[0])
-        # one un-timed check that the plan equals the fused C-ABI forward
+        run_steps(fwd, full, args.warmup)
+        if tail_fwd is not None:
+            tail_fwd.run(*tail[0])
+        # one un-timed check: the timed path, the module's forward and the
+        # stage-by-stage plan give bitwise the same logits
+        y_fwd = fwd.run(cand, clk).clone()
+        y_mod = model.forward_ids(cand, clk, proj_mode=mode)
         y_plan = plan.run(cand, clk).clone()
-        y_fwd = model.forward_ids(cand, clk, proj_mode=mode)
-        same = bool(torch.equal(y_plan, y_fwd))
-        events = [[torch.cuda.Event(enable_timing=True) for _ in range(n_st + 1)] for _ in range(steps)]
+        same = bool(torch.equal(y_fwd, y_mod)) and (args.unfused or bool(torch.equal(y_fwd, y_plan)))
+        events = (fwd.make_events(steps) if not args.unfused else
+                  [[torch.cuda.Event(enable_timing=True) for _ in range(n_st + 1)] for _ in range(steps)])
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        run_plan_steps(plan, full, steps, events)
-        if args.stream and tail_plan is not None and steps == len(full):
-            tail_plan.run(*tail[0])
+        run_steps(fwd, full, steps, events)
+        if args.stream and tail_fwd is not None and steps == len(full):
+            tail_fwd.run(*tail[0])
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -356,9 +371,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    stage_ms = {st: 0.0 for st in plan.stages}
+    stage_ms = {st: 0.0 for st in stages}
     for ev in events:
-        for i, st in enumerate(plan.stages):
+        for i, st in enumerate(stages):
             stage_ms[st] += ev[i].elapsed_time(ev[i + 1])
     stage_ms = {st: v / steps for st, v in stage_ms.items()}
     # titles the news tail encodes per step: with padding-title dedupe (library
@@ -371,7 +386,12 @@ def main():
     grp = torch.nn.functional.pad((all_titles != 0).any(-1), (0, (-n_titles) % 4)).view(-1, 4).any(-1)
     n_pad_groups = int((~grp).sum())
     n_enc = 4 * (grp.numel() - n_pad_groups + (1 if n_pad_groups else 0))
-    work = plan.work(titles_encoded=n_enc)
+    # clicked rows the UserEncoder projects: the copied padding rows are skipped
+    n_clk = clk.shape[0] * N_CLICKED
+    clk_pad_groups = int((~grp[: (n_clk + 3) // 4]).sum())
+    n_user = n_clk - 4 * max(clk_pad_groups - 1, 0) if not args.unfused else n_clk
+    work = plan.work(titles_encoded=n_enc if not args.unfused else n_all_titles(B),
+                     user_rows_projected=n_user)
     dom = max(stage_ms, key=stage_ms.get)
     w = work[dom]
     t_dom = stage_ms[dom] / 1e3
@@ -443,34 +463,38 @@ def main():
                              "copied to the other all-padding groups (bitwise identical logits; "
                              "no_title_dedupe below times every title encoded)"},
         "stages_ms": {st: round(v, 4) for st, v in stage_ms.items()},
-        "plan_equals_nrms_forward": same,
+        "user_rows_projected": n_user,
+        "timed_path": "nrms_forward_timed (one C-ABI call per step)" if not args.unfused
+                      else "ForwardPlan stage kernels (--unfused)",
+        "forward_paths_bitwise_equal": same,
     }
     if rank == 0 and world == 1 and not args.no_extras and not args.stream:
         out["gather_roofline"] = gather_hbm(device)
         out["news_encoder_cfg2"] = news_encoder_cfg2(model, device)
-        if args.proj == "folded":
-            dplan = ForwardPlan(model, B, C, N_CLICKED, L, proj_mode=Nat.NRMS_PROJ_DIRECT,
-                                fused=not args.unfused)
+        if args.proj == "folded" and not args.unfused:
+            dfwd = TimedForward(model, B, C, N_CLICKED, L, proj_mode=Nat.NRMS_PROJ_DIRECT)
             with torch.no_grad():
-                dplan.run(cand, clk)
-                dms = _time_launches(lambda: dplan.run(cand, clk), 10, device)
+                y_d = dfwd.run(cand, clk).clone()
+                dms = _time_launches(lambda: dfwd.run(cand, clk), 10, device)
             lib = Nat.load()
-            lib.nrms_set_title_dedupe(0)
+            prev = lib.nrms_set_title_dedupe(0)
             try:
                 with torch.no_grad():
-                    plan.run(cand, clk)
-                    nms = _time_launches(lambda: plan.run(cand, clk), 10, device)
+                    y_n = fwd.run(cand, clk).clone()
+                    nms = _time_launches(lambda: fwd.run(cand, clk), 10, device)
             finally:
-                lib.nrms_set_title_dedupe(1)
+                lib.nrms_set_title_dedupe(prev)
             out["no_title_dedupe"] = {
                 "ms_per_step": round(nms, 4), "impressions_per_s": round(B / (nms / 1e3), 1),
-                "note": "every all-padding history title encoded separately (nrms_set_title_dedupe(0)), "
-                        "bitwise the same logits"}
+                "logits_bitwise_equal": bool(torch.equal(y_n, y_fwd)),
+                "note": "every title encoded and every clicked row projected separately "
+                        "(nrms_set_title_dedupe(0))"}
             out["direct_projection"] = {
                 "ms_per_step": round(dms, 4), "impressions_per_s": round(B / (dms / 1e3), 1),
+                "max_rel_diff_vs_folded": float(((y_d - y_fwd).norm(dim=1) / y_fwd.norm(dim=1)).max()),
                 "note": "per-token Q|K|V projection (no vocabulary folding): the work SURVEY §8d's "
                         "789.6 MFLOP/impression unit describes"}
-            del dplan
+            del dfwd
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stream:
         cb, parity = cpu_baseline(model, cand, clk)
         out["cpu_baseline"] = cb

@@ -44,7 +44,9 @@ extern "C" {
 /* 2: nrms_user_encode takes batch / row strides; nrms_adam_step_multi takes a
  *    host descriptor array (no device table, no total_blocks); q|k|v buffers
  *    carry a row stride (nrms_qkv_row_stride). */
-#define NRMS_ABI_VERSION 2
+/* 3: nrms_forward_timed / nrms_forward_stage_name; nrms_forward's workspace
+ *    holds the UserEncoder row list (nrms_forward_workspace_size grew). */
+#define NRMS_ABI_VERSION 3
 
 typedef enum {
   NRMS_OK = 0,
@@ -251,8 +253,12 @@ int32_t nrms_impression_metrics(const float* scores, const int32_t* labels,
                                 hipStream_t stream);
 
 /* NRMS.forward (src/model/NRMS/__init__.py:19-48), eval mode:
- * cand_ids[B, C, L], clicked_ids[B, N, L] -> logits[B, C]. All B*(C+N) titles
- * are encoded (forward semantics), then the user vector and the scores. */
+ * cand_ids[B, C, L], clicked_ids[B, N, L] -> logits[B, C]. Every one of the
+ * B*(C+N) titles gets its news vector (forward semantics), then the user
+ * vector and the scores. With title dedupe (nrms_set_title_dedupe, default)
+ * all-padding history titles are encoded once per batch and copied, and the
+ * UserEncoder projects their q|k|v rows once as well; the logits are bitwise
+ * those of encoding and projecting every title. */
 size_t nrms_forward_workspace_size(int64_t B, int32_t C, int32_t N, int32_t L, int64_t V,
                                    int32_t D, int32_t proj_mode);
 int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_t B, int32_t C,
@@ -260,6 +266,20 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
                      const nrms_encoder_weights_t* news_w, const nrms_encoder_weights_t* user_w,
                      int32_t proj_mode, float* logits, void* workspace, size_t workspace_bytes,
                      hipStream_t stream);
+
+/* nrms_forward with per-stage timing: stage_events[i] (n_events =
+ * NRMS_FORWARD_STAGES + 1 caller-created HIP events, or n_events = 0 for none)
+ * is recorded on the stream before stage i and the last one after the final
+ * stage. Stages: nrms_forward_stage_name(0 .. NRMS_FORWARD_STAGES - 1) =
+ * qkv_news (Q|K|V projection), news_fused (news attention + additive pooling,
+ * incl. the padding-group and recheck launches), qkv_user, user_fused, score. */
+#define NRMS_FORWARD_STAGES 5
+int32_t nrms_forward_timed(const int64_t* cand_ids, const int64_t* clicked_ids, int64_t B, int32_t C,
+                           int32_t N, int32_t L, const float* table, int64_t V,
+                           const nrms_encoder_weights_t* news_w, const nrms_encoder_weights_t* user_w,
+                           int32_t proj_mode, float* logits, void* workspace, size_t workspace_bytes,
+                           hipStream_t stream, hipEvent_t* stage_events, int32_t n_events);
+const char* nrms_forward_stage_name(int32_t stage);
 
 /* ---------------------------------------------------------------------------
  * Training kernels: the train-mode forward pieces and the backward of the path

@@ -115,11 +115,12 @@ size_t news_bytes(const NewsSizes& z) {
 int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                         int64_t n_seq_a, const int64_t* ids_b, int64_t n_seq, int32_t L,
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
-                        hipStream_t s, float* wap = nullptr) {
+                        hipStream_t s, float* wap = nullptr, bool* deduped = nullptr) {
   const int D = w->d_model;
+  if (deduped) *deduped = false;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
     return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
-                             w->q_add, wap, out, s);
+                             w->q_add, wap, out, s, -1, deduped);
   if (ldq != 3 * (int64_t)D) return NRMS_ERR_UNSUPPORTED;   // stage kernels: packed rows
   int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
@@ -394,14 +395,18 @@ size_t nrms_forward_workspace_size(int64_t B, int32_t C, int32_t N, int32_t L, i
   const int64_t n_all = B * (C + N);
   return nrms_news_encode_workspace_size(n_all, L, V, D, proj_mode) +
          align_up((size_t)n_all * D * 4) + align_up((size_t)B * D * 4) +
-         nrms_user_encode_workspace_size(B, N, D);
+         nrms_user_encode_workspace_size(B, N, D) + align_up((size_t)B * N * 8) + align_up(4);
 }
 
-int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_t B, int32_t C,
+namespace {
+
+// nrms_forward / nrms_forward_timed. ev (optional, NRMS_FORWARD_STAGES + 1
+// events): recorded on the stream before each stage and after the last.
+int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_t B, int32_t C,
                      int32_t N, int32_t L, const float* table, int64_t V,
                      const nrms_encoder_weights_t* news_w, const nrms_encoder_weights_t* user_w,
                      int32_t proj_mode, float* logits, void* workspace, size_t workspace_bytes,
-                     hipStream_t stream) {
+                     hipStream_t stream, hipEvent_t* ev) {
   if (B < 0 || C < 0 || N <= 0 || L <= 0 || V <= 0) return NRMS_ERR_INVALID_ARG;
   if (int32_t st = shape_ok(news_w)) return st;
   if (int32_t st = shape_ok(user_w)) return st;
@@ -413,6 +418,7 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   const bool folded = use_folded(proj_mode, n_all * L, V);
   const NewsSizes z = news_sizes(n_all, L, V, D, folded);
   const int64_t ld = news_ld(news_w, L);
+  const int64_t uld = user_ld(user_w, N);
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
   float* qkv = cv.floats(z.qkv);
   float* ctx = cv.floats(z.ctx);
@@ -420,16 +426,27 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   float* wap = cv.floats(z.wap);
   float* news = cv.floats((size_t)n_all * D);   // [clicked B*N | candidates B*C] x D
   float* user = cv.floats((size_t)B * D);
+  float* uqkv = cv.floats((size_t)n_clk * (size_t)uld);
+  float* uctx = cv.floats((size_t)n_clk * D);
+  float* uscores = cv.floats((size_t)n_clk);
+  float* uwap = cv.floats(fused_user_packed_b_floats());
+  int64_t* ulist = reinterpret_cast<int64_t*>(cv.floats((size_t)n_clk * 2));
+  int32_t* ucount = reinterpret_cast<int32_t*>(cv.floats(1));
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
-  char* user_ws = static_cast<char*>(workspace) + cv.off;
-  const size_t user_ws_bytes = workspace_bytes - cv.off;
+  auto rec = [&](int i) -> int32_t {
+    if (ev && hipEventRecord(ev[i], stream) != hipSuccess) return launch_status();
+    return NRMS_OK;
+  };
 
   int32_t st;
+  bool deduped = false;
+  if ((st = rec(0))) return st;
   if (folded) {
     st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(news_w), 3 * D, qkv, ld, stream);
     if (st) return st;
+    if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
-                         news, stream, wap);
+                         news, stream, wap, &deduped);
   } else {
     st = launch_gemm_store(table, V, clicked_ids, n_clk * L, D, qkv_rows(news_w), 3 * D, qkv, ld,
                            stream);
@@ -437,14 +454,71 @@ int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
     st = launch_gemm_store(table, V, cand_ids, B * C * L, D, qkv_rows(news_w), 3 * D,
                            qkv + (size_t)n_clk * L * ld, ld, stream);
     if (st) return st;
+    if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, n_all * L, nullptr, n_all, nullptr, n_all, L, news_w, ctx,
                          scores, news, stream, wap);
   }
   if (st) return st;
-  st = nrms_user_encode(news, B, N, (int64_t)N * D, D, user_w, user, user_ws, user_ws_bytes, stream);
+  if ((st = rec(2))) return st;
+  // UserEncoder (src/model/NRMS/user_encoder.py:15-26) over the clicked news
+  // vectors. After a deduplicating news launch, the clicked titles of copied
+  // all-padding groups carry bitwise copies of the rep group's vectors, so
+  // their q|k|v rows are the rep rows': only the other rows are projected
+  // (row-list GEMM) and the fused tail reads copied positions from the rep
+  // rows. Bitwise the same logits as projecting every row.
+  const bool user_fused = fused_user_supported(N, D, user_w->n_heads, user_w->query_dim) &&
+                          ((uintptr_t)user % 16) == 0;
+  const bool user_dedupe = deduped && user_fused && gemm_arith() != NRMS_GEMM_F32;
+  PaddingGroups pg{nullptr, nullptr};
+  if (user_dedupe) {
+    pg = fused_news_padding_groups(wap, n_all);
+    if ((st = launch_user_row_list(pg, n_clk, ulist, ucount, stream))) return st;
+    st = launch_gemm_store_list(news, n_clk, ulist, ucount, n_clk, D, qkv_rows(user_w), 3 * D, uqkv,
+                                uld, stream);
+  } else {
+    st = launch_gemm_store(news, n_clk, nullptr, n_clk, D, qkv_rows(user_w), 3 * D, uqkv, uld, stream);
+  }
   if (st) return st;
-  return launch_score(news + (size_t)n_clk * D, B, C, (int64_t)C * D, D, user, D, D, logits,
-                      stream);
+  if ((st = rec(3))) return st;
+  if (user_fused)
+    st = launch_fused_user(uqkv, uld, B, N, user_w->w_add, user_w->b_add, user_w->q_add, uwap, user,
+                           stream, user_dedupe ? &pg : nullptr);
+  else
+    st = encode_from_qkv(uqkv, uld, n_clk, nullptr, B, nullptr, B, N, user_w, uctx, uscores, user,
+                         stream);
+  if (st) return st;
+  if ((st = rec(4))) return st;
+  st = launch_score(news + (size_t)n_clk * D, B, C, (int64_t)C * D, D, user, D, D, logits, stream);
+  if (st) return st;
+  return rec(5);
+}
+
+}  // namespace
+
+int32_t nrms_forward(const int64_t* cand_ids, const int64_t* clicked_ids, int64_t B, int32_t C,
+                     int32_t N, int32_t L, const float* table, int64_t V,
+                     const nrms_encoder_weights_t* news_w, const nrms_encoder_weights_t* user_w,
+                     int32_t proj_mode, float* logits, void* workspace, size_t workspace_bytes,
+                     hipStream_t stream) {
+  return forward_impl(cand_ids, clicked_ids, B, C, N, L, table, V, news_w, user_w, proj_mode, logits,
+                      workspace, workspace_bytes, stream, nullptr);
+}
+
+int32_t nrms_forward_timed(const int64_t* cand_ids, const int64_t* clicked_ids, int64_t B, int32_t C,
+                           int32_t N, int32_t L, const float* table, int64_t V,
+                           const nrms_encoder_weights_t* news_w, const nrms_encoder_weights_t* user_w,
+                           int32_t proj_mode, float* logits, void* workspace, size_t workspace_bytes,
+                           hipStream_t stream, hipEvent_t* stage_events, int32_t n_events) {
+  if (n_events != 0 && (n_events != NRMS_FORWARD_STAGES + 1 || !stage_events))
+    return NRMS_ERR_INVALID_ARG;
+  return forward_impl(cand_ids, clicked_ids, B, C, N, L, table, V, news_w, user_w, proj_mode, logits,
+                      workspace, workspace_bytes, stream, n_events ? stage_events : nullptr);
+}
+
+const char* nrms_forward_stage_name(int32_t i) {
+  static const char* names[NRMS_FORWARD_STAGES] = {"qkv_news", "news_fused", "qkv_user", "user_fused",
+                                                   "score"};
+  return (i >= 0 && i < NRMS_FORWARD_STAGES) ? names[i] : nullptr;
 }
 
 

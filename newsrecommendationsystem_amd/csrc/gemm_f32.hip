@@ -245,7 +245,9 @@ __device__ __forceinline__ void split4(const float4 v, bf16x4& h, bf16x4& m, bf1
   l = __builtin_bit_cast(bf16x4, make_uint2(l0, l1));
 }
 
-template <int TNW, int BMT>
+// SCATTER: output row m goes to Y row row_ids[m] (row-list GEMM: the rows to
+// project are listed, each written back in place).
+template <int TNW, int BMT, bool SCATTER>
 __device__ __forceinline__ void gemm_x6_tile(
     const float* __restrict__ X, int64_t n_rows_x, ARows ar, const int64_t* __restrict__ row_ids,
     int64_t M, int K, const WeightRows& wr, int N, float* __restrict__ Y, int64_t ldy,
@@ -385,7 +387,7 @@ __device__ __forceinline__ void gemm_x6_tile(
       for (int r = 0; r < 4; ++r) {
         const int64_t row = row_base + 16 * mt + r;
         if (row < M) {
-          float* yp = Y + row * ldy + col;
+          float* yp = Y + (SCATTER ? row_ids[row] : row) * ldy + col;
           *yp = (wr.accumulate ? *yp : 0.f) + acc[mt][nt][r] + bias;
         }
       }
@@ -395,19 +397,34 @@ __device__ __forceinline__ void gemm_x6_tile(
 // 192-wide column tiles; a last partial tile of <= 160 columns (N = 900:
 // 4 x 192 + 132) runs the 160-wide instantiation so its two wave columns
 // stay balanced (5 + 4 live N tiles instead of 6 + 3).
+// Row-list mode (SCATTER): row_ids lists the rows to project, m_dev their
+// count (device memory, written by an earlier launch; the grid is sized for
+// M rows and the blocks past the count exit at once).
+template <bool SCATTER>
 __global__ __launch_bounds__(kThreads, 3) void gemm_x6_kernel(
     const float* __restrict__ X, int64_t n_rows_x, ARows ar, const int64_t* __restrict__ row_ids,
-    int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy, int n_col_tiles) {
+    int64_t M, int K, WeightRows wr, int N, float* __restrict__ Y, int64_t ldy, int n_col_tiles,
+    const int32_t* __restrict__ m_dev) {
   __shared__ __attribute__((aligned(16))) __bf16 As[3 * XBM * XLD];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[3 * 192 * XLD];
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  // list mode: only the first ceil(count / 64) row tiles are live; the blocks
+  // past them exit, and the XCD remap runs over the live range only (over the
+  // whole grid it would pack every live tile onto the first XCDs)
+  int nwg = gridDim.x;
+  if constexpr (SCATTER) {
+    const int64_t mc = *m_dev;
+    M = mc < M ? mc : M;
+    nwg = (int)((M + XBM - 1) / XBM) * n_col_tiles;
+    if ((int)blockIdx.x >= nwg) return;
+  }
+  const int wg = xcd_remap(blockIdx.x, nwg);
   const int ct = wg % n_col_tiles;
   const int64_t m0 = (int64_t)(wg / n_col_tiles) * XBM;
   const int n0 = ct * 192;
   if (N - n0 > 160)
-    gemm_x6_tile<6, XBM>(X, n_rows_x, ar, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
+    gemm_x6_tile<6, XBM, SCATTER>(X, n_rows_x, ar, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
   else
-    gemm_x6_tile<5, XBM>(X, n_rows_x, ar, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
+    gemm_x6_tile<5, XBM, SCATTER>(X, n_rows_x, ar, row_ids, M, K, wr, N, Y, ldy, m0, n0, As, Bs);
 }
 
 constexpr int TN_STORE = 12;     // BN = 192: N = 900 -> 4 column tiles of 192 + one of 144
@@ -439,8 +456,8 @@ int32_t launch_gemm_store_rows(const float* X, int64_t n_rows_x, ARows ar, const
     const int64_t nrt = (M + XBM - 1) / XBM;
     const int64_t blocks = nrt * nct;
     if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(gemm_x6_kernel, dim3((unsigned)blocks), dim3(kThreads), 0, s, X, n_rows_x,
-                       ar, row_ids, M, K, w, N, Y, ldy, nct);
+    hipLaunchKernelGGL(gemm_x6_kernel<false>, dim3((unsigned)blocks), dim3(kThreads), 0, s, X, n_rows_x,
+                       ar, row_ids, M, K, w, N, Y, ldy, nct, (const int32_t*)nullptr);
     return launch_status();
   }
   const int nct = (N + 16 * TN_STORE - 1) / (16 * TN_STORE);
@@ -458,6 +475,22 @@ int32_t launch_gemm_store_rows(const float* X, int64_t n_rows_x, ARows ar, const
     hipLaunchKernelGGL((gemm_xwt_f32_kernel<TN_STORE, TN_STORE, false>), dim3((unsigned)blocks),
                        dim3(kThreads), 0, s, X, n_rows_x, ar, row_ids, M, K, w, N, Y, ldy,
                        (const float*)nullptr, (float*)nullptr, nct);
+  return launch_status();
+}
+
+int32_t launch_gemm_store_list(const float* X, int64_t n_rows_x, const int64_t* rows,
+                               const int32_t* count_dev, int64_t max_rows, int K, const WeightRows& w,
+                               int N, float* Y, int64_t ldy, hipStream_t s) {
+  if (max_rows == 0) return NRMS_OK;
+  if (K % 4 != 0 || ((uintptr_t)X % 16) != 0 || !rows || !count_dev) return NRMS_ERR_UNSUPPORTED;
+  for (int i = 0; i < w.nseg; ++i)
+    if (((uintptr_t)w.w[i] % 16) != 0) return NRMS_ERR_UNSUPPORTED;
+  if (gemm_arith() == NRMS_GEMM_F32) return NRMS_ERR_UNSUPPORTED;   // callers project every row instead
+  const int nct = (N + 191) / 192;
+  const int64_t blocks = (max_rows + XBM - 1) / XBM * nct;
+  if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(gemm_x6_kernel<true>, dim3((unsigned)blocks), dim3(kThreads), 0, s, X, n_rows_x,
+                     contiguous_rows(K), rows, max_rows, K, w, N, Y, ldy, nct, count_dev);
   return launch_status();
 }
 

@@ -269,6 +269,33 @@ __global__ __launch_bounds__(256) void broadcast_padding_kernel(const uint8_t* _
       reinterpret_cast<const float4*>(out + (r * FT + (s % FT)) * FD)[c];
 }
 
+// The clicked rows m < n_rows (titles 0 .. n_rows - 1 of the launch) whose
+// q|k|v the UserEncoder needs: all but the rows of all-padding groups other
+// than rep, whose news vectors are copies of rep's slot m % 4 (the UserEncoder
+// reads those rows from 4 rep + m % 4 instead). Appended in any order (vector
+// atomics, one per wave); the count must start at 0.
+__global__ __launch_bounds__(256) void user_row_list_kernel(const uint8_t* __restrict__ pad_group,
+                                                            const int32_t* __restrict__ rep,
+                                                            int64_t n_rows, int64_t* __restrict__ list,
+                                                            int32_t* __restrict__ count) {
+  // one atomic per block (per-wave atomics on the one counter serialised: 11 us)
+  __shared__ int wcount[4], wbase[4];
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t g = m >> 2;
+  const bool keep = m < n_rows && !(pad_group[g] && g != (int64_t)*rep);
+  const uint64_t ballot = __ballot(keep);
+  if (lane == 0) wcount[w] = __popcll(ballot);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    int b = tot ? atomicAdd(count, tot) : 0;
+    for (int i = 0; i < 4; ++i) { wbase[i] = b; b += wcount[i]; }
+  }
+  __syncthreads();
+  if (keep) list[wbase[w] + __popcll(ballot & ((1ull << lane) - 1))] = m;
+}
+
 // Rows near fp32 overflow (nrms_common.hpp, kExpRecheck). The main pass
 // (EXACT = false) takes the fast exp everywhere and appends the title groups
 // that need the reference's exp to `list` (one entry per flagging wave;
@@ -893,6 +920,9 @@ static std::atomic<int> g_title_dedupe{[] {
   return (e && e[0] == '0') ? 0 : 1;
 }()};
 int title_dedupe() { return g_title_dedupe.load(std::memory_order_relaxed); }
+static bool dedupe_applies(int dedupe, const int64_t* ids_a, const int64_t* ids_b) {
+  return dedupe && ids_a != nullptr && (((uintptr_t)ids_a | (uintptr_t)(ids_b ? ids_b : ids_a)) % 16) == 0;
+}
 int set_title_dedupe(int on) { return g_title_dedupe.exchange(on ? 1 : 0); }
 
 bool fused_news_supported(int L, int D, int H, int Q) {
@@ -909,7 +939,8 @@ unsigned long long* g_fused_dbg = nullptr;   // set by profiles/probes/news_vari
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
-                          float* out, hipStream_t s) {
+                          float* out, hipStream_t s, int dedupe_setting, bool* deduped) {
+  if (deduped) *deduped = false;
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
   if (ldq < ROW || ldq % 4) return NRMS_ERR_UNSUPPORTED;   // float4 q / k slices
@@ -930,8 +961,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   int32_t* glist = rcount + 4 + 4 * n_groups;
   uint8_t* pad_group = reinterpret_cast<uint8_t*>(glist + n_groups);
   // padding-group dedupe needs the token ids (gathered rows), 16-B aligned id rows
-  const bool dedupe = title_dedupe() && ids_a != nullptr &&
-                      (((uintptr_t)ids_a | (uintptr_t)(ids_b ? ids_b : ids_a)) % 16) == 0;
+  const bool dedupe = dedupe_applies(dedupe_setting < 0 ? title_dedupe() : dedupe_setting, ids_a, ids_b);
   const GroupList gl{dedupe ? glist : nullptr, rcount + 1, rcount + 2};
   if (x6) {
     const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
@@ -973,6 +1003,24 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
     hipLaunchKernelGGL(broadcast_padding_kernel, dim3((unsigned)((nt4 + 255) / 256)), dim3(256), 0, s,
                        pad_group, rcount + 2, n_titles, out);
   }
+  const int32_t st = launch_status();
+  if (st == NRMS_OK && deduped) *deduped = dedupe;
+  return st;
+}
+
+PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles) {
+  const int64_t n_groups = (n_titles + FT - 1) / FT;
+  int32_t* rcount = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
+  int32_t* glist = rcount + 4 + 4 * n_groups;
+  return PaddingGroups{reinterpret_cast<const uint8_t*>(glist + n_groups), rcount + 2};
+}
+
+int32_t launch_user_row_list(const PaddingGroups& pg, int64_t n_rows, int64_t* list, int32_t* count,
+                             hipStream_t s) {
+  if (hipMemsetAsync(count, 0, sizeof(int32_t), s) != hipSuccess) return launch_status();
+  if (n_rows == 0) return NRMS_OK;
+  hipLaunchKernelGGL(user_row_list_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s,
+                     pg.pad_group, pg.rep, n_rows, list, count);
   return launch_status();
 }
 

@@ -162,6 +162,11 @@ int32_t launch_gather(const int64_t* ids, int64_t n_tok, const float* table, int
 int32_t launch_gemm_store(const float* X, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
                           int K, const WeightRows& w, int N, float* Y, int64_t ldy,
                           hipStream_t s);
+// Row-list GEMM (split arithmetic only): Y[rows[m]] = X[rows[m]] W^T + b for
+// m < *count_dev (device memory); the grid covers max_rows.
+int32_t launch_gemm_store_list(const float* X, int64_t n_rows_x, const int64_t* rows,
+                               const int32_t* count_dev, int64_t max_rows, int K, const WeightRows& w,
+                               int N, float* Y, int64_t ldy, hipStream_t s);
 // Same, A rows addressed through `ar` (strided [B, N, K] input views).
 int32_t launch_gemm_store_rows(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids,
                                int64_t M, int K, const WeightRows& w, int N, float* Y,
@@ -203,11 +208,20 @@ int32_t launch_adam_multi(const nrms_adam_tensor_t* ts, int n, float lr, float b
 int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,
                     float b2, float eps, int64_t step, hipStream_t s);
 
+// Device-side padding classification a deduplicating fused-news launch left
+// in its workspace: pad_group[g] = 1 for all-padding 4-title groups, and title
+// 4g + t of such a group (g != *rep) carries a copy of title 4 rep + t.
+struct PaddingGroups {
+  const uint8_t* pad_group;
+  const int32_t* rep;
+};
 size_t fused_user_packed_b_floats();
 bool fused_user_supported(int L, int D, int H, int Q);
+// pg (optional): rows m = b L + i of copied padding titles (see
+// PaddingGroups) are read from 4 rep + m % 4.
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
-                          hipStream_t s);
+                          hipStream_t s, const PaddingGroups* pg = nullptr);
 // Process-wide switch (news_fused.hip): encode one all-padding title per
 // batch and broadcast its vector (nrms_set_title_dedupe; NRMS_DEDUPE=0 in the
 // environment turns it off).
@@ -217,10 +231,18 @@ int set_title_dedupe(int on);
 // workspace of launch_fused_news: packed W_add, special rows, recheck list
 size_t fused_news_workspace_floats(int64_t n_titles);
 bool fused_news_supported(int L, int D, int H, int Q);
+// dedupe_setting: -1 = the process-wide nrms_set_title_dedupe setting, else
+// 0 / 1; *deduped (optional) tells whether the padding groups were classified
+// (fused_news_padding_groups is then valid until the workspace is reused).
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
-                          float* out, hipStream_t s);
+                          float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr);
+PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles);
+// The rows m < n_rows of titles not copied from rep (the UserEncoder's rows to
+// project), appended to list in any order; *count set on the stream.
+int32_t launch_user_row_list(const PaddingGroups& pg, int64_t n_rows, int64_t* list, int32_t* count,
+                             hipStream_t s);
 int32_t launch_score_pairs(const float* news, int64_t n_news, const float* user, int64_t n_users,
                            const int64_t* news_idx, const int64_t* user_idx, int64_t n_pairs,
                            int D, float* out, hipStream_t s);

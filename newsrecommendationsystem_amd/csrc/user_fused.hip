@@ -90,7 +90,8 @@ __device__ __forceinline__ int ukpos(int k) {
 template <int MODE, int LMAX, int NT>
 __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     const float* __restrict__ qkv, int64_t ldq, int L, const float* __restrict__ WaP,
-    const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out) {
+    const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
+    PaddingGroups pg) {
   static_assert(NT >= UH * LMAX, "one (head, query) task per thread");
   constexpr int NW = NT / 64;
   constexpr int NTPW = (UNT + NW - 1) / NW;            // N-tiles per wave
@@ -102,14 +103,21 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   const int64_t s = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const float* rows = qkv + s * L * ldq;   // q|k|v rows at stride ldq floats
+  // q|k|v row of position i (stride ldq floats); with pg, a position holding a
+  // copied padding title reads the row of the title it copies
+  const int32_t rep = pg.pad_group ? *pg.rep : 0;
+  auto row = [&](int i) -> const float* {
+    int64_t m = s * L + i;
+    if (pg.pad_group && pg.pad_group[m >> 2] && (m >> 2) != rep) m = 4 * (int64_t)rep + (m & 3);
+    return qkv + m * ldq;
+  };
 
   // ---------------- 0. stage K|V (all loads in flight at once), q slices ----------------
   const bool has = tid < UH * L;
   const int h = has ? tid / L : 0, qi = has ? tid - h * L : 0;
   float q[UDK];
   {
-    const float4* qp = reinterpret_cast<const float4*>(rows + (size_t)qi * ldq + UDK * h);
+    const float4* qp = reinterpret_cast<const float4*>(row(qi) + UDK * h);
 #pragma unroll
     for (int t = 0; t < UDK / 4; ++t) {
       const float4 v = qp[t];
@@ -122,7 +130,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     for (int k = 0; k < PER; ++k) {
       const int e = tid + k * NT;
       const int i = e / KV4, c = e - i * KV4;
-      buf[k] = e < L * KV4 ? *reinterpret_cast<const float4*>(rows + (size_t)i * ldq + UD + 4 * c)
+      buf[k] = e < L * KV4 ? *reinterpret_cast<const float4*>(row(i) + UD + 4 * c)
                            : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
@@ -373,21 +381,23 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 
 template <int MODE, int LMAX, int NT>
 int32_t launch_user_inst(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
-                         const float* b_add, const float* q_add, float* out, hipStream_t s) {
+                         const float* b_add, const float* q_add, float* out, hipStream_t s,
+                         PaddingGroups pg) {
   const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64) * 4;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>), (int)lds);
   hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
-                     ldq, L, wap, b_add, q_add, out);
+                     ldq, L, wap, b_add, q_add, out, pg);
   return launch_status();
 }
 
 template <int MODE>
 int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
-                         const float* b_add, const float* q_add, float* out, hipStream_t s) {
-  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
-  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
-  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
-  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
+                         const float* b_add, const float* q_add, float* out, hipStream_t s,
+                         PaddingGroups pg) {
+  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
+  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
+  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
+  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
 }
 
 }  // namespace
@@ -400,7 +410,8 @@ bool fused_user_supported(int L, int D, int H, int Q) {
 
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
-                          hipStream_t s) {
+                          hipStream_t s, const PaddingGroups* pgp) {
+  const PaddingGroups pg = pgp ? *pgp : PaddingGroups{nullptr, nullptr};
   if (B == 0) return NRMS_OK;
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16 || ldq < 3 * UD || ldq % 4)
@@ -409,8 +420,8 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
   const int npk = x6 ? UKS * UNT * 64 * 8 : UWAP1;
   hipLaunchKernelGGL(pack_user_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap, x6);
   if (int32_t st = launch_status()) return st;
-  if (x6) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
-  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s);
+  if (x6) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
+  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
 }
 
 }  // namespace nrms

@@ -128,13 +128,17 @@ class ForwardPlan:
 
     # Algorithmic work per launch of each stage (SURVEY §8d conventions:
     # GEMMs 2·M·N·K; bytes = operands the stage must read + results it writes).
-    def work(self, titles_encoded=None):
+    def work(self, titles_encoded=None, user_rows_projected=None):
         """titles_encoded: titles the fused news tail actually encodes (with
-        padding-title dedupe: the non-padding titles + 1); default all."""
+        padding-title dedupe: the titles of the non-padding 4-title groups + one
+        padding group); user_rows_projected: clicked rows the UserEncoder's
+        Q|K|V GEMM projects (with dedupe: all but the copied padding rows);
+        default all."""
         B, C, Nc, L, D, V = self.B, self.C, self.N, self.L, self.D, self.V
         Q, H, dk = 200, 15, D // 15
         n_all, n_clk = B * (C + Nc), B * Nc
         n_enc = n_all if titles_encoded is None else titles_encoded
+        n_up = n_clk if user_rows_projected is None else user_rows_projected
         att_flop = lambda seqs, l: seqs * H * 2 * (2 * l * l * dk)
         qkv_m = V if self.folded else n_all * L
         return {
@@ -152,7 +156,7 @@ class ForwardPlan:
                                + 4 * (n_all * D + Q * D),
                                split=dict(attention=att_flop(n_enc, L), gemm=2 * n_enc * L * D * Q,
                                           pool=2 * n_enc * L * D)),
-            "qkv_user": dict(flop=2 * n_clk * D * 3 * D, bytes=4 * (n_clk * 4 * D + 3 * D * D)),
+            "qkv_user": dict(flop=2 * n_up * D * 3 * D, bytes=4 * (n_up * 4 * D + 3 * D * D)),
             "mhsa_user": dict(flop=att_flop(B, Nc), bytes=4 * n_clk * 4 * D),
             "addscore_user": dict(flop=2 * n_clk * D * Q, bytes=4 * (n_clk * (D + 1) + Q * D)),
             "pool_user": dict(flop=2 * n_clk * D, bytes=4 * (n_clk * (D + 1) + B * D)),
@@ -161,3 +165,46 @@ class ForwardPlan:
                                bytes=4 * (n_clk * 3 * D + B * D + Q * D)),
             "score": dict(flop=2 * B * C * D, bytes=4 * (B * C * D + B * D + B * C)),
         }
+
+
+class TimedForward:
+    """The product path, nrms_forward, with per-stage HIP events
+    (nrms_forward_timed): one C-ABI call per step from a preallocated
+    workspace; event i is recorded on the launch stream before stage i
+    (stages = nrms_forward_stage_name) and the last after the final stage.
+    Unlike ForwardPlan it takes nrms_forward's internal shortcuts (the
+    UserEncoder's row-list projection after padding-title dedupe)."""
+
+    def __init__(self, model, B, C, n_clicked, L, proj_mode=N.NRMS_PROJ_FOLDED):
+        ne = model.news_encoder
+        self.dev = ne.word_embedding.weight.device
+        self.table = ne.table()
+        self.V, self.D = self.table.shape
+        self.B, self.C, self.N, self.L, self.mode = B, C, n_clicked, L, proj_mode
+        lib = N.load()
+        nb = lib.nrms_forward_workspace_size(B, C, n_clicked, L, self.V, self.D, proj_mode)
+        self.ws = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+        self.logits = torch.empty(B, C, dtype=torch.float32, device=self.dev)
+        self.wn, self._keep_n = ne.weights()
+        self.wu, self._keep_u = model.user_encoder.weights()
+        self.stages = [lib.nrms_forward_stage_name(i).decode() for i in range(N.NRMS_FORWARD_STAGES)]
+
+    def make_events(self, n_steps):
+        """n_steps lists of len(stages)+1 timing events, created (recorded once)."""
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(self.stages) + 1)]
+               for _ in range(n_steps)]
+        for row in evs:
+            for e in row:
+                e.record()
+        torch.cuda.synchronize(self.dev)
+        return evs
+
+    def run(self, cand_ids, clicked_ids, events=None):
+        arr = None
+        if events is not None:
+            arr = (ctypes.c_void_p * len(events))(*[ctypes.c_void_p(e.cuda_event) for e in events])
+        N.call("nrms_forward_timed", N.ptr(cand_ids), N.ptr(clicked_ids), self.B, self.C, self.N,
+               self.L, N.ptr(self.table), self.V, ctypes.byref(self.wn), ctypes.byref(self.wu),
+               self.mode, N.ptr(self.logits), N.ptr(self.ws), self.ws.numel(),
+               N.stream_handle(self.dev), arr, len(events) if events is not None else 0)
+        return self.logits

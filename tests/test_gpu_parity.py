@@ -629,3 +629,31 @@ def test_padding_title_dedupe_is_bitwise_identical(device, pad_frac, gemm_mode):
     if pad.any():   # one vector per slot; slots agree to fp32 rounding
         vp = outs[1][1][pad.to(device)]
         assert float((vp - vp[:1]).abs().max()) <= 1e-6 * float(vp.abs().max())
+
+
+def test_forward_timed_matches_forward_and_records_stages(device):
+    """nrms_forward_timed (bench.py's timed step): bitwise the logits of
+    nrms_forward / NRMS.forward_ids and of the stage-by-stage ForwardPlan, with
+    the five stage events recorded in order (positive, summing to the span)."""
+    from newsrecommendationsystem_amd import _native as N
+    from newsrecommendationsystem_amd.pipeline import ForwardPlan, TimedForward
+    V, B = 3000, 70
+    sd = W.nrms_state(91, V)
+    m = _module(sd, V, device)
+    cand, clk, _ = W.impressions(91, 5, B, V)
+    c, k = torch.from_numpy(cand).to(device), torch.from_numpy(clk).to(device)
+    fwd = TimedForward(m, B, 5, 50, 20)
+    assert fwd.stages == ["qkv_news", "news_fused", "qkv_user", "user_fused", "score"]
+    ev = fwd.make_events(1)[0]
+    with torch.no_grad():
+        y = fwd.run(c, k, ev).clone()
+        ref = m.forward_ids(c, k)
+        plan = ForwardPlan(m, B, 5, 50, 20).run(c, k).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref) and torch.equal(y, plan)
+    ms = [ev[i].elapsed_time(ev[i + 1]) for i in range(5)]
+    assert all(t > 0 for t in ms), ms
+    assert abs(sum(ms) - ev[0].elapsed_time(ev[5])) < 1e-2
+    lib = N.load()
+    assert lib.nrms_forward_timed(None, None, B, 5, 50, 20, None, V, None, None, 2, None, None, 0,
+                                  None, None, 3) == N.NRMS_ERR_INVALID_ARG
