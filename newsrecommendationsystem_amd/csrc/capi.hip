@@ -395,7 +395,7 @@ size_t nrms_forward_workspace_size(int64_t B, int32_t C, int32_t N, int32_t L, i
   const int64_t n_all = B * (C + N);
   return nrms_news_encode_workspace_size(n_all, L, V, D, proj_mode) +
          align_up((size_t)n_all * D * 4) + align_up((size_t)B * D * 4) +
-         nrms_user_encode_workspace_size(B, N, D) + align_up((size_t)B * N * 8) + align_up(4);
+         nrms_user_encode_workspace_size(B, N, D) + align_up((size_t)B * N * 8);
 }
 
 namespace {
@@ -431,7 +431,6 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   float* uscores = cv.floats((size_t)n_clk);
   float* uwap = cv.floats(fused_user_packed_b_floats());
   int64_t* ulist = reinterpret_cast<int64_t*>(cv.floats((size_t)n_clk * 2));
-  int32_t* ucount = reinterpret_cast<int32_t*>(cv.floats(1));
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   auto rec = [&](int i) -> int32_t {
     if (ev && hipEventRecord(ev[i], stream) != hipSuccess) return launch_status();
@@ -469,12 +468,12 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   const bool user_fused = fused_user_supported(N, D, user_w->n_heads, user_w->query_dim) &&
                           ((uintptr_t)user % 16) == 0;
   const bool user_dedupe = deduped && user_fused && gemm_arith() != NRMS_GEMM_F32;
-  PaddingGroups pg{nullptr, nullptr};
+  PaddingGroups pg{nullptr, nullptr, nullptr};
   if (user_dedupe) {
     pg = fused_news_padding_groups(wap, n_all);
-    if ((st = launch_user_row_list(pg, n_clk, ulist, ucount, stream))) return st;
-    st = launch_gemm_store_list(news, n_clk, ulist, ucount, n_clk, D, qkv_rows(user_w), 3 * D, uqkv,
-                                uld, stream);
+    if ((st = launch_user_row_list(pg, n_clk, ulist, stream))) return st;
+    st = launch_gemm_store_list(news, n_clk, ulist, pg.user_count, n_clk, D, qkv_rows(user_w), 3 * D,
+                                uqkv, uld, stream);
   } else {
     st = launch_gemm_store(news, n_clk, nullptr, n_clk, D, qkv_rows(user_w), 3 * D, uqkv, uld, stream);
   }

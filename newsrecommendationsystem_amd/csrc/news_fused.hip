@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
                                                               float* __restrict__ WaP,
                                                               int32_t* __restrict__ recheck_count) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx < 4)   // [recheck count, group-list count, rep, 0]
+  if (idx < 4)   // [recheck count, group-list count, rep, user row-list count]
     recheck_count[idx] = idx == 2 ? INT32_MAX : 0;
   if (idx >= WAP_FLOATS + SPECIAL_FLOATS) return;
   if (idx >= WAP_FLOATS) {
@@ -218,41 +218,47 @@ struct GroupList {
   const int32_t* rep;   // INT32_MAX: no all-padding group
 };
 
-// One thread per group: classify (all 80 ids zero; slots past n_titles count as
-// padding) and append the others to the list; one atomic per wave (vector
-// atomics only).
+// One thread per title (10 x 16-B id loads), the 4 lanes of a group combined
+// by a ballot: classify each group (all 80 ids zero; slots past n_titles count
+// as padding) and append the others to the list; one atomic per block.
 __global__ __launch_bounds__(256) void classify_groups_kernel(RowMap rm, int64_t n_groups,
                                                               int32_t* __restrict__ list,
                                                               int32_t* __restrict__ count,
                                                               int32_t* __restrict__ rep,
                                                               uint8_t* __restrict__ pad_group) {
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const bool live = g < n_groups;
-  bool pad = false;
-  if (live) {
-    int64_t any = 0;
-    for (int t = 0; t < FT; ++t) {
-      const int64_t s = g * FT + t;
-      if (s >= rm.n_titles) break;
-      const int64_t* ids = rm.ids_of(s);
+  __shared__ int wcount[4], wbase[4], wrep[4];
+  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;   // title
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int64_t any = 0;
+  if (s < rm.n_titles) {
+    const int64_t* ids = rm.ids_of(s);
 #pragma unroll
-      for (int i = 0; i < FL; i += 2) {
-        const int4 v = *reinterpret_cast<const int4*>(ids + i);   // 16-B aligned id rows (checked)
-        any |= (int64_t)(v.x | v.y | v.z | v.w);
-      }
+    for (int i = 0; i < FL; i += 2) {
+      const int4 v = *reinterpret_cast<const int4*>(ids + i);   // 16-B aligned id rows (checked)
+      any |= (int64_t)(v.x | v.y | v.z | v.w);
     }
-    pad = any == 0;
-    pad_group[g] = pad ? 1 : 0;
   }
-  const uint64_t keep = __ballot(live && !pad);
-  const uint64_t pads = __ballot(live && pad);
-  int base = 0;
-  if (lane == 0 && keep) base = atomicAdd(count, __popcll(keep));
-  base = __shfl(base, 0);
-  if (live && !pad) list[base + __popcll(keep & ((1ull << lane) - 1))] = (int32_t)g;
-  if (pads != 0 && lane == 0)
-    atomicMin(rep, (int32_t)((int64_t)blockIdx.x * 256 + (threadIdx.x & ~63) + __ffsll((long long)pads) - 1));
+  const uint64_t real = __ballot(any != 0);
+  const int64_t g = s >> 2;
+  const bool lead = (lane & 3) == 0 && g < n_groups;
+  const bool pad = ((real >> (lane & ~3)) & 0xFull) == 0;
+  if (lead) pad_group[g] = pad ? 1 : 0;
+  const uint64_t keep = __ballot(lead && !pad);
+  const uint64_t pads = __ballot(lead && pad);
+  if (lane == 0) {
+    wcount[w] = __popcll(keep);
+    wrep[w] = pads ? (int32_t)((s >> 2) + ((__ffsll((long long)pads) - 1) >> 2)) : INT32_MAX;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int r = min(min(wrep[0], wrep[1]), min(wrep[2], wrep[3]));
+    if (r != INT32_MAX) atomicMin(rep, r);
+    const int tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    int b = tot ? atomicAdd(count, tot) : 0;
+    for (int i = 0; i < 4; ++i) { wbase[i] = b; b += wcount[i]; }
+  }
+  __syncthreads();
+  if (lead && !pad) list[wbase[w] + __popcll(keep & ((1ull << lane) - 1))] = (int32_t)g;
 }
 
 // out[s] = out[4 rep + s % 4] for every title s of the other all-padding groups.
@@ -907,7 +913,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 }  // namespace
 
 // packed W_add + special rows, then int32 [recheck count, group-list count,
-// rep, 0], the recheck list (4 per group), the group list, pad_group bytes
+// rep, user row-list count] (zeroed / rep = INT32_MAX by the pack kernel of
+// every launch), the recheck list (4 per group), the group list, pad_group
+// bytes
 static size_t fused_news_list_offset() { return (size_t)WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS; }
 size_t fused_news_workspace_floats(int64_t n_titles) {
   const int64_t n_groups = (n_titles + FT - 1) / FT;
@@ -986,8 +994,8 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   const int64_t blocks = n_groups < n_cu ? n_groups : n_cu;   // persistent: one workgroup per CU
   RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows};
   if (dedupe) {
-    hipLaunchKernelGGL(classify_groups_kernel, dim3((unsigned)((n_groups + 255) / 256)), dim3(256), 0, s,
-                       rm, n_groups, glist, rcount + 1, rcount + 2, pad_group);
+    hipLaunchKernelGGL(classify_groups_kernel, dim3((unsigned)((4 * n_groups + 255) / 256)), dim3(256), 0,
+                       s, rm, n_groups, glist, rcount + 1, rcount + 2, pad_group);
     if (int32_t st = launch_status()) return st;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, gl, ws,
@@ -1012,13 +1020,12 @@ PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles) {
   const int64_t n_groups = (n_titles + FT - 1) / FT;
   int32_t* rcount = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
   int32_t* glist = rcount + 4 + 4 * n_groups;
-  return PaddingGroups{reinterpret_cast<const uint8_t*>(glist + n_groups), rcount + 2};
+  return PaddingGroups{reinterpret_cast<const uint8_t*>(glist + n_groups), rcount + 2, rcount + 3};
 }
 
-int32_t launch_user_row_list(const PaddingGroups& pg, int64_t n_rows, int64_t* list, int32_t* count,
-                             hipStream_t s) {
-  if (hipMemsetAsync(count, 0, sizeof(int32_t), s) != hipSuccess) return launch_status();
+int32_t launch_user_row_list(const PaddingGroups& pg, int64_t n_rows, int64_t* list, hipStream_t s) {
   if (n_rows == 0) return NRMS_OK;
+  int32_t* count = pg.user_count;
   hipLaunchKernelGGL(user_row_list_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s,
                      pg.pad_group, pg.rep, n_rows, list, count);
   return launch_status();

@@ -211,9 +211,11 @@ int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, flo
 // Device-side padding classification a deduplicating fused-news launch left
 // in its workspace: pad_group[g] = 1 for all-padding 4-title groups, and title
 // 4g + t of such a group (g != *rep) carries a copy of title 4 rep + t.
+// user_count: the launch's (zeroed) slot for launch_user_row_list's count.
 struct PaddingGroups {
   const uint8_t* pad_group;
   const int32_t* rep;
+  int32_t* user_count;
 };
 size_t fused_user_packed_b_floats();
 bool fused_user_supported(int L, int D, int H, int Q);
@@ -240,9 +242,8 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
                           float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr);
 PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles);
 // The rows m < n_rows of titles not copied from rep (the UserEncoder's rows to
-// project), appended to list in any order; *count set on the stream.
-int32_t launch_user_row_list(const PaddingGroups& pg, int64_t n_rows, int64_t* list, int32_t* count,
-                             hipStream_t s);
+// project), appended to list in any order; their count in *pg.user_count.
+int32_t launch_user_row_list(const PaddingGroups& pg, int64_t n_rows, int64_t* list, hipStream_t s);
 int32_t launch_score_pairs(const float* news, int64_t n_news, const float* user, int64_t n_users,
                            const int64_t* news_idx, const int64_t* user_idx, int64_t n_pairs,
                            int D, float* out, hipStream_t s);
