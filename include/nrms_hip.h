@@ -46,7 +46,9 @@ extern "C" {
  *    carry a row stride (nrms_qkv_row_stride). */
 /* 3: nrms_forward_timed / nrms_forward_stage_name; nrms_forward's workspace
  *    holds the UserEncoder row list (nrms_forward_workspace_size grew). */
-#define NRMS_ABI_VERSION 3
+/* 4: nrms_qkv_project_ws; the encode / forward workspaces hold the split
+ *    Q|K|V weight (their *_workspace_size functions grew). */
+#define NRMS_ABI_VERSION 4
 
 typedef enum {
   NRMS_OK = 0,
@@ -140,6 +142,17 @@ int32_t nrms_qkv_row_stride(int32_t D);
 int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
                          const nrms_encoder_weights_t* w, float* qkv, int64_t ld_qkv,
                          hipStream_t stream);
+
+/* Same rows, bitwise, through the workspace: for the NRMS shape (D = 300,
+ * split arithmetic) the weight is split into bf16 planes once per call
+ * (workspace) and one persistent workgroup per CU keeps a 64-row tile of x
+ * resident in LDS while it streams the planes from L2 — the projection the
+ * encode / forward entry points use. Other shapes / NRMS_GEMM_F32: as
+ * nrms_qkv_project. */
+size_t nrms_qkv_project_workspace_size(int32_t D);
+int32_t nrms_qkv_project_ws(const float* x, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
+                            const nrms_encoder_weights_t* w, float* qkv, int64_t ld_qkv,
+                            void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* Multi-head raw-exp self-attention over sequences of length L
  * (ScaledDotProductAttention, multihead_self.py:15-23, heads concatenated

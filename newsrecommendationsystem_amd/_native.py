@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NRMS_LIB_PATH") or os.path.join(_PKG, "libnrms_hip.so")   # override: A/B builds
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
 NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32, NRMS_GEMM_SPLIT_F16X3 = 0, 1, 2
@@ -46,6 +46,8 @@ SIGNATURES = {
     "nrms_embedding_gather": (_i32, [_p, _i64, _p, _i64, _i32, _p, _p]),
     "nrms_qkv_row_stride": (_i32, [_i32]),
     "nrms_qkv_project": (_i32, [_p, _i64, _p, _i64, _EW, _p, _i64, _p]),
+    "nrms_qkv_project_workspace_size": (_sz, [_i32]),
+    "nrms_qkv_project_ws": (_i32, [_p, _i64, _p, _i64, _EW, _p, _i64, _p, _sz, _p]),
     "nrms_self_attention": (_i32, [_p, _i64, _p, _i64, _p, _i64, _i32, _EW, _p, _p]),
     "nrms_additive_attention": (_i32, [_p, _i64, _i32, _EW, _p, _p, _p]),
     "nrms_additive_scores": (_i32, [_p, _i64, _EW, _p, _p]),

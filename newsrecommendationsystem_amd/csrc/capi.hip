@@ -99,15 +99,34 @@ bool use_folded(int32_t mode, int64_t n_tok, int64_t V) {
 
 // Per-stage sizes (floats).
 struct NewsSizes {
-  size_t qkv, ctx, scores, wap;
+  size_t qkv, ctx, scores, wap, pack;
 };
 NewsSizes news_sizes(int64_t n_titles, int32_t L, int64_t V, int32_t D, bool folded) {
   const size_t ntok = (size_t)n_titles * (size_t)L;
   return {(folded ? (size_t)V : ntok) * (size_t)qkv_row_stride(D), ntok * (size_t)D, ntok,
-          fused_news_workspace_floats(n_titles)};
+          fused_news_workspace_floats(n_titles), proj_x6_pack_floats()};
 }
 size_t news_bytes(const NewsSizes& z) {
-  return align_up(z.qkv * 4) + align_up(z.ctx * 4) + align_up(z.scores * 4) + align_up(z.wap * 4);
+  return align_up(z.qkv * 4) + align_up(z.ctx * 4) + align_up(z.scores * 4) + align_up(z.wap * 4) +
+         align_up(z.pack * 4);
+}
+
+// Q|K|V projection of the encoders: the pre-split-W kernel (proj_x6.hip) when
+// the shape and arithmetic allow, packing w into `pack` first unless the
+// caller already did (packed = true); the staged GEMM otherwise. Bitwise the
+// same rows either way. list_count non-null: row-list mode (launch_gemm_store_list).
+int32_t project_qkv(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
+                    const nrms_encoder_weights_t* w, float* pack, bool packed, float* Y, int64_t ld,
+                    hipStream_t s, const int32_t* list_count = nullptr) {
+  const int D = w->d_model;
+  const WeightRows wr = qkv_rows(w);
+  if (pack && proj_x6_supported(D, 3 * D, wr)) {
+    if (!packed)
+      if (int32_t st = launch_proj_x6_pack(wr, pack, nullptr, nullptr, s)) return st;
+    return launch_proj_x6(X, n_rows_x, ar, row_ids, M, pack, Y, ld, list_count, s);
+  }
+  if (list_count) return launch_gemm_store_list(X, n_rows_x, row_ids, list_count, M, D, wr, 3 * D, Y, ld, s);
+  return launch_gemm_store_rows(X, n_rows_x, ar, row_ids, M, D, wr, 3 * D, Y, ld, s);
 }
 
 // attention + additive pooling from projected rows (shared by news and user
@@ -181,6 +200,26 @@ int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_id
   if (ld_qkv == 0) ld_qkv = 3 * D;
   if (ld_qkv < 3 * D) return NRMS_ERR_INVALID_ARG;
   return launch_gemm_store(x, n_rows_x, row_ids, M, D, qkv_rows(w), 3 * D, qkv, ld_qkv, stream);
+}
+
+size_t nrms_qkv_project_workspace_size(int32_t D) {
+  return D > 0 ? align_up(proj_x6_pack_floats() * 4) : 0;
+}
+
+int32_t nrms_qkv_project_ws(const float* x, int64_t n_rows_x, const int64_t* row_ids, int64_t M,
+                            const nrms_encoder_weights_t* w, float* qkv, int64_t ld_qkv, void* workspace,
+                            size_t workspace_bytes, hipStream_t stream) {
+  if (M < 0 || n_rows_x < 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (M > 0 && (!x || !qkv)) return NRMS_ERR_INVALID_ARG;
+  const int D = w->d_model;
+  if (ld_qkv == 0) ld_qkv = 3 * D;
+  if (ld_qkv < 3 * D) return NRMS_ERR_INVALID_ARG;
+  if (M == 0) return NRMS_OK;
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* pack = cv.floats(proj_x6_pack_floats());
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  return project_qkv(x, n_rows_x, contiguous_rows(D), row_ids, M, w, pack, false, qkv, ld_qkv, stream);
 }
 
 int32_t nrms_self_attention(const float* qkv, int64_t n_rows_qkv, const int64_t* tok_ids,
@@ -268,17 +307,18 @@ int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const 
   float* ctx = cv.floats(z.ctx);
   float* scores = cv.floats(z.scores);
   float* wap = cv.floats(z.wap);
+  float* pack = cv.floats(z.pack);
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   int32_t st;
   if (folded) {
     // Vocabulary-level projection: one GEMM over the table, then rows gathered by id.
-    st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(w), 3 * D, qkv, ld, stream);
+    st = project_qkv(table, V, contiguous_rows(D), nullptr, V, w, pack, false, qkv, ld, stream);
     if (st) return st;
     return encode_from_qkv(qkv, ld, V, ids, n_titles, nullptr, n_titles, L, w, ctx, scores, out,
                            stream, wap);
   }
   // Per-token projection with the embedding gather fused into the A-operand load.
-  st = launch_gemm_store(table, V, ids, n_titles * L, D, qkv_rows(w), 3 * D, qkv, ld, stream);
+  st = project_qkv(table, V, contiguous_rows(D), ids, n_titles * L, w, pack, false, qkv, ld, stream);
   if (st) return st;
   return encode_from_qkv(qkv, ld, n_titles * L, nullptr, n_titles, nullptr, n_titles, L, w, ctx,
                          scores, out, stream, wap);
@@ -314,7 +354,7 @@ size_t nrms_user_encode_workspace_size(int64_t B, int32_t N, int32_t D) {
   if (B < 0 || N <= 0 || D <= 0) return 0;
   const size_t rows = (size_t)B * N;
   return align_up(rows * (size_t)qkv_row_stride(D) * 4) + align_up(rows * D * 4) + align_up(rows * 4) +
-         align_up(fused_user_packed_b_floats() * 4);
+         align_up(fused_user_packed_b_floats() * 4) + align_up(proj_x6_pack_floats() * 4);
 }
 
 size_t nrms_user_attention_pool_workspace_size(int64_t B, int32_t N, int32_t D) {
@@ -352,13 +392,13 @@ int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N, int64_t str
   float* ctx = cv.floats((size_t)rows * D);
   float* scores = cv.floats((size_t)rows);
   float* wap = cv.floats(fused_user_packed_b_floats());
+  float* pack = cv.floats(proj_x6_pack_floats());
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   // the [B, N, D] view is read in place (e.g. the transpose(0, 1) of
   // src/evaluate.py:220-224: stride_b = D, stride_n = B * D)
   const ARows ar = (stride_b == (int64_t)N * D && stride_n == D) ? contiguous_rows(D)
                                                                  : ARows{N, stride_b, stride_n};
-  int32_t st = launch_gemm_store_rows(clicked, rows, ar, nullptr, rows, D, qkv_rows(w), 3 * D, qkv,
-                                      ld, stream);
+  int32_t st = project_qkv(clicked, rows, ar, nullptr, rows, w, pack, false, qkv, ld, stream);
   if (st) return st;
   if (fused_user_supported(N, D, w->n_heads, w->query_dim) && ((uintptr_t)out % 16) == 0)
     return launch_fused_user(qkv, ld, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
@@ -424,12 +464,14 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   float* ctx = cv.floats(z.ctx);
   float* scores = cv.floats(z.scores);
   float* wap = cv.floats(z.wap);
+  float* pack = cv.floats(z.pack);
   float* news = cv.floats((size_t)n_all * D);   // [clicked B*N | candidates B*C] x D
   float* user = cv.floats((size_t)B * D);
   float* uqkv = cv.floats((size_t)n_clk * (size_t)uld);
   float* uctx = cv.floats((size_t)n_clk * D);
   float* uscores = cv.floats((size_t)n_clk);
   float* uwap = cv.floats(fused_user_packed_b_floats());
+  float* upack = cv.floats(proj_x6_pack_floats());
   int64_t* ulist = reinterpret_cast<int64_t*>(cv.floats((size_t)n_clk * 2));
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   auto rec = [&](int i) -> int32_t {
@@ -440,18 +482,22 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   int32_t st;
   bool deduped = false;
   if ((st = rec(0))) return st;
+  // both weight sets split once, in one launch
+  const WeightRows nwr = qkv_rows(news_w), uwr = qkv_rows(user_w);
+  const bool packed = proj_x6_supported(D, 3 * D, nwr);
+  if (packed && (st = launch_proj_x6_pack(nwr, pack, &uwr, upack, stream))) return st;
   if (folded) {
-    st = launch_gemm_store(table, V, nullptr, V, D, qkv_rows(news_w), 3 * D, qkv, ld, stream);
+    st = project_qkv(table, V, contiguous_rows(D), nullptr, V, news_w, pack, packed, qkv, ld, stream);
     if (st) return st;
     if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
                          news, stream, wap, &deduped);
   } else {
-    st = launch_gemm_store(table, V, clicked_ids, n_clk * L, D, qkv_rows(news_w), 3 * D, qkv, ld,
-                           stream);
+    st = project_qkv(table, V, contiguous_rows(D), clicked_ids, n_clk * L, news_w, pack, packed, qkv, ld,
+                     stream);
     if (st) return st;
-    st = launch_gemm_store(table, V, cand_ids, B * C * L, D, qkv_rows(news_w), 3 * D,
-                           qkv + (size_t)n_clk * L * ld, ld, stream);
+    st = project_qkv(table, V, contiguous_rows(D), cand_ids, B * C * L, news_w, pack, packed,
+                     qkv + (size_t)n_clk * L * ld, ld, stream);
     if (st) return st;
     if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, n_all * L, nullptr, n_all, nullptr, n_all, L, news_w, ctx,
@@ -472,10 +518,10 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   if (user_dedupe) {
     pg = fused_news_padding_groups(wap, n_all);
     if ((st = launch_user_row_list(pg, n_clk, ulist, stream))) return st;
-    st = launch_gemm_store_list(news, n_clk, ulist, pg.user_count, n_clk, D, qkv_rows(user_w), 3 * D,
-                                uqkv, uld, stream);
+    st = project_qkv(news, n_clk, contiguous_rows(D), ulist, n_clk, user_w, upack, packed, uqkv, uld, stream,
+                     pg.user_count);
   } else {
-    st = launch_gemm_store(news, n_clk, nullptr, n_clk, D, qkv_rows(user_w), 3 * D, uqkv, uld, stream);
+    st = project_qkv(news, n_clk, contiguous_rows(D), nullptr, n_clk, user_w, upack, packed, uqkv, uld, stream);
   }
   if (st) return st;
   if ((st = rec(3))) return st;

@@ -171,6 +171,17 @@ int32_t launch_gemm_store_list(const float* X, int64_t n_rows_x, const int64_t* 
 int32_t launch_gemm_store_rows(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids,
                                int64_t M, int K, const WeightRows& w, int N, float* Y,
                                int64_t ldy, hipStream_t s);
+// Q|K|V projection with W split once per call (proj_x6.hip): K = 300, N = 900,
+// split arithmetic, no accumulate. The pack (proj_x6_pack_floats() floats,
+// 16-B aligned) is written by launch_proj_x6_pack for one or two weight sets
+// and read by launch_proj_x6; bitwise the result of launch_gemm_store_rows /
+// launch_gemm_store_list. m_dev non-null: row-list mode (row_ids lists the
+// rows, *m_dev their count; outputs written in place).
+size_t proj_x6_pack_floats();
+bool proj_x6_supported(int K, int N, const WeightRows& w);
+int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, hipStream_t s);
+int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
+                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, hipStream_t s);
 int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
                                    const float* b, const float* q, int N, float* score,
                                    hipStream_t s);

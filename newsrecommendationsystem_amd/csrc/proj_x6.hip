@@ -1,0 +1,332 @@
+// Q|K|V projection Y = X[row(m)] · [Wq; Wk; Wv]^T + [bq; bk; bv] for the
+// NRMS shape (K = D = 300, N = 3D = 900; multihead_self.py:53-58) on the
+// split-bf16 x6 arithmetic, with the weight split once per call.
+//
+// gemm_x6_kernel (gemm_f32.hip) stages A and W chunks through LDS and splits
+// both while staging: for a 64 x 192 tile the 192 W rows are split again for
+// every 64 rows of A, three times the splitting the A tile itself needs, and
+// that VALU work is what bounds it (4-5 VALU per MFMA, PMC). Here:
+//   * proj_x6_pack_kernel splits W once per call into MFMA B fragments,
+//     [k-step][N tile][plane][lane][8 bf16] (1.75 MB, stays in every XCD's
+//     L2), plus the bias row;
+//   * one persistent workgroup per CU keeps a 64-row A tile resident in LDS as
+//     three bf16 planes (split once, 125 KB) and computes its outputs in three
+//     20-tile column ranges (items), each wave 5 N tiles x 4 M tiles, streaming
+//     the B fragments from L2 through a buffer resource (lane / N tile in one
+//     VGPR offset, k-step / plane in the SGPR offset: no per-load address
+//     registers in the unrolled 10-k-step mainloop);
+//   * the next row tile's A rows are loaded into registers during the last
+//     k-step of the tile's last item, split into LDS behind one barrier pair.
+// Each output tile accumulates exactly the MFMA sequence of gemm_x6_kernel —
+// the same k-steps, fragment K order and product order (lo·hi, mid·mid, hi·lo,
+// mid·hi, hi·mid, hi·hi), then (0 + acc) + bias — so the two kernels agree
+// bitwise (tests/test_gpu_parity.py compares them).
+#include "nrms_common.hpp"
+
+#include <type_traits>
+
+namespace nrms {
+namespace {
+
+constexpr int PK = 300, PN = 900;
+constexpr int PKS = 10;                          // k-steps of 32 (K padded to 320)
+constexpr int PKP = PKS * 32;                    // 320
+constexpr int PNT = (PN + 15) / 16;              // 57 N tiles (the last: 4 live columns)
+constexpr int PM = 64;                           // A rows per tile
+constexpr int PMT = PM / 16;                     // 4 M tiles
+constexpr int PTW = 5;                           // N tiles per wave per item
+constexpr int PRANGE = 4 * PTW;                  // N tiles per item
+constexpr int PNR = (PNT + PRANGE - 1) / PRANGE; // items per row tile (3)
+static_assert(PNT - (PNR - 1) * PRANGE >= 16, "every wave of the last range owns 4 or 5 tiles");
+// LDS row: [hi 320 | mid 320 | lo 320 | pad 16] bf16 = 1,952 B = 488 dwords
+// (= 40 mod 64): the 16-row x 4-kq fragment reads cover all 64 banks once.
+constexpr int PRB = 3 * PKP + 16;
+constexpr size_t P_LDS = (size_t)PM * PRB * 2 + PM * sizeof(int64_t);
+static_assert(P_LDS <= 160 * 1024, "LDS");
+constexpr int PACK_BF16 = PKS * PNT * 3 * 512;   // B fragments
+constexpr int PTRASH = 16 * PNT;                 // floats: target of the stores of rows past M
+// + bias row (0 past N), zero row, NaN row, trash line
+constexpr int PACK_FLOATS = PACK_BF16 / 2 + PNT * 16 + 2 * PKP + PTRASH;
+constexpr int A_F4 = PM * PK / 4;                // float4 pieces of an A tile (4,800)
+constexpr int A_PASSES = (A_F4 + 255) / 256;     // 19 per thread
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)x;
+  const float r = x - (float)hi;
+  mid = (__bf16)r;
+  lo = (__bf16)(r - (float)mid);
+}
+
+// [ks][nt][plane][lane][8]: plane of W[16 nt + (lane & 15)][32 ks + 8 (lane >> 4) + i]
+// (0 past N or K), then bias[16 PNT], a zero row and a NaN row (the A rows of
+// rows past M / of invalid ids). blockIdx.y selects the weight set.
+__global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, WeightRows w1, float* __restrict__ d0,
+                                                           float* __restrict__ d1) {
+  const WeightRows& w = blockIdx.y ? w1 : w0;
+  float* dst = blockIdx.y ? d1 : d0;
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  constexpr int NE = PKS * PNT * 512;
+  if (idx < NE) {
+    const int i = idx & 7, lane = (idx >> 3) & 63, t = idx >> 9;
+    const int nt = t % PNT, ks = t / PNT;
+    const int n = 16 * nt + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + i;
+    float v = 0.f;
+    if (n < PN && k < PK) {
+      const int seg = n / w.seg_rows;
+      v = w.w[seg][(int64_t)(n - seg * w.seg_rows) * PK + k];
+    }
+    __bf16 hi, mid, lo;
+    split3(v, hi, mid, lo);
+    __bf16* o = reinterpret_cast<__bf16*>(dst) + (int64_t)t * 3 * 512 + lane * 8 + i;
+    o[0] = hi;
+    o[512] = mid;
+    o[1024] = lo;
+  } else if (idx < NE + PNT * 16) {
+    const int c = idx - NE;
+    float b = 0.f;
+    if (c < PN) {
+      const int seg = c / w.seg_rows;
+      b = w.b[seg] ? w.b[seg][c - seg * w.seg_rows] : 0.f;
+    }
+    dst[PACK_BF16 / 2 + c] = b;
+  } else if (idx < NE + PNT * 16 + 2 * PKP) {
+    const int c = idx - NE - PNT * 16;
+    dst[PACK_BF16 / 2 + PNT * 16 + c] = c < PKP ? 0.f : qnan();
+  }
+}
+
+// SCATTER: output row m goes to Y row row_ids[m] (row-list mode; the count is
+// *m_dev, written by an earlier launch). Otherwise row_ids (optional) only
+// gathers the A rows (the fused embedding gather of the per-token mode).
+template <bool SCATTER>
+__global__ __launch_bounds__(256, 1) void proj_x6_kernel(const float* __restrict__ X, int64_t n_rows_x, ARows ar,
+                                                        const int64_t* __restrict__ row_ids, int64_t M,
+                                                        const float* __restrict__ packed, float* __restrict__ Y,
+                                                        int64_t ldy, const int32_t* __restrict__ m_dev) {
+  extern __shared__ __attribute__((aligned(16))) float lds_f[];
+  __bf16* As = reinterpret_cast<__bf16*>(lds_f);
+  int64_t* orow = reinterpret_cast<int64_t*>(As + PM * PRB);   // output row offset (-1: no row)
+
+  if constexpr (SCATTER) {
+    const int64_t mc = *m_dev;
+    M = mc < M ? mc : M;
+  }
+  const int64_t n_items = (M + PM - 1) / PM * PNR;
+  const int64_t i0 = (int64_t)blockIdx.x * n_items / gridDim.x;
+  const int64_t i1 = ((int64_t)blockIdx.x + 1) * n_items / gridDim.x;
+  if (i0 >= i1) return;
+
+  const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int lm = lane & 15, kq = lane >> 4;
+
+  // K padding: columns 300..319 of every plane stay zero for the whole launch
+  for (int e = tid; e < PM * 3 * ((PKP - PK) / 4); e += 256) {
+    const int r = e / (3 * ((PKP - PK) / 4)), rem = e - r * (3 * ((PKP - PK) / 4));
+    const int pl = rem / ((PKP - PK) / 4), c = rem - pl * ((PKP - PK) / 4);
+    *reinterpret_cast<uint2*>(As + r * PRB + pl * PKP + PK + 4 * c) = make_uint2(0u, 0u);
+  }
+
+  // A tile staging: thread (row ar_ = tid / 4, quarter q = tid % 4) moves the
+  // float4 pieces q, q + 4, .. of one row (19 per thread, the last for q < 3),
+  // from one source pointer per row tile: the row itself, the pack's zero row
+  // (past M) or its NaN row (invalid id: the row becomes NaN, as gemm_x6_kernel)
+  const int ar_ = tid >> 2, aq = tid & 3;
+  const float* zero_row = packed + PACK_FLOATS - PTRASH - 2 * PKP;
+  const float* nan_row = zero_row + PKP;
+  struct ASrc {
+    const float* p;
+    int64_t o;   // output row offset (-1: no row)
+  };
+  auto a_src = [&](int64_t rt) __attribute__((always_inline)) -> ASrc {
+    const int64_t m = rt * PM + ar_;
+    if (m >= M) return ASrc{zero_row, -1};
+    const int64_t id = row_ids ? row_ids[m] : m;
+    const int64_t o = (SCATTER ? id : m) * ldy;
+    return ASrc{(uint64_t)id < (uint64_t)n_rows_x ? X + ar.offset(id) : nan_row, o};
+  };
+  float4 ra[A_PASSES];
+  auto load_a = [&](const float* src) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < A_PASSES; ++j) {
+      const int c4 = aq + 4 * j < PK / 4 ? aq + 4 * j : PK / 4 - 1;   // (the q = 3 lane of the last pass: unused)
+      ra[j] = *reinterpret_cast<const float4*>(src + 4 * c4);
+    }
+  };
+  auto store_a = [&](int64_t o) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < A_PASSES; ++j) {
+      const int c4 = aq + 4 * j;
+      if (c4 < PK / 4) {
+        uint32_t h0, m0, l0, h1, m1, l1;
+        split3x2(ra[j].x, ra[j].y, h0, m0, l0);
+        split3x2(ra[j].z, ra[j].w, h1, m1, l1);
+        __bf16* d = As + ar_ * PRB + 4 * c4;
+        *reinterpret_cast<uint2*>(d) = make_uint2(h0, h1);
+        *reinterpret_cast<uint2*>(d + PKP) = make_uint2(m0, m1);
+        *reinterpret_cast<uint2*>(d + 2 * PKP) = make_uint2(l0, l1);
+      }
+    }
+    if (aq == 0) orow[ar_] = o;
+  };
+
+  {
+    const ASrc a0 = a_src(i0 / PNR);
+    load_a(a0.p);
+    store_a(a0.o);
+  }
+  __syncthreads();
+
+  const __amdgpu_buffer_rsrc_t brs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(packed), 0, PACK_BF16 * 2, 0x00020000);
+  const float* bias = packed + PACK_BF16 / 2;
+  float* trash = const_cast<float*>(packed) + PACK_FLOATS - PTRASH;   // stores of rows past M
+  // A fragments (16x16x32): lane holds A[row lm + 16 mt][32 ks + 8 kq .. + 7] of each plane
+  const __bf16* Ab = As + lm * PRB + 8 * kq;
+
+  for (int64_t it = i0; it < i1; ++it) {
+    const int64_t rt = it / PNR;
+    const int rg = (int)(it - rt * PNR);
+    const bool restage = it + 1 < i1 && (it + 1) / PNR != rt;   // workgroup-uniform
+    ASrc an{zero_row, -1};
+    if (restage) an = a_src(rt + 1);   // (its id load completes behind the mainloop)
+    // the range's tiles split evenly over the waves (N = 900: 5/5/5/5, 5/5/5/5, 4/4/4/5)
+    const int r0 = rg * PRANGE, nr = (r0 + PRANGE < PNT ? r0 + PRANGE : PNT) - r0;
+    const int t0 = r0 + w * nr / 4;
+    const int live = r0 + (w + 1) * nr / 4 - t0;
+
+    auto body = [&](auto cc) __attribute__((always_inline)) {
+      constexpr int C = decltype(cc)::value;
+      floatx4 acc[PMT][C];
+#pragma unroll
+      for (int mt = 0; mt < PMT; ++mt)
+#pragma unroll
+        for (int j = 0; j < C; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+      int bvoff[C];
+      float bj[C];
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        bvoff[j] = lane * 16 + (t0 + j) * 3 * 1024;
+        bj[j] = bias[16 * (t0 + j) + lm];   // (0 past N)
+      }
+      // plane-major: the hi planes (first product's B) arrive first
+      auto load_b = [&](int ks, bf16x8 (&dst)[C][3]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+          for (int j = 0; j < C; ++j)
+            dst[j][pl] = __builtin_bit_cast(
+                bf16x8, __builtin_amdgcn_raw_buffer_load_b128(brs, bvoff[j], (ks * PNT * 3 + pl) * 1024, 0));
+      };
+      auto kstep = [&](int ks, const bf16x8 (&bb)[C][3]) __attribute__((always_inline)) {
+        bf16x8 a[PMT][3];
+#pragma unroll
+        for (int pl = 2; pl >= 0; --pl)
+#pragma unroll
+          for (int mt = 0; mt < PMT; ++mt)
+            a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * PRB + pl * PKP + 32 * ks);
+#define NRMS_PX6(PA, PB)                                                                              \
+  _Pragma("unroll") for (int j = 0; j < C; ++j)                                                       \
+  _Pragma("unroll") for (int mt = 0; mt < PMT; ++mt)                                                  \
+      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);
+        NRMS_PX6(2, 0) NRMS_PX6(1, 1) NRMS_PX6(0, 2) NRMS_PX6(1, 0) NRMS_PX6(0, 1) NRMS_PX6(0, 0)
+#undef NRMS_PX6
+      };
+      // two B buffers in turn, each k-step's loads fenced where they are issued
+      bf16x8 b0[C][3], b1[C][3];
+      load_b(0, b0);
+#pragma unroll
+      for (int ks = 0; ks < PKS; ks += 2) {
+        load_b(ks + 1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+        kstep(ks, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        if (ks + 2 < PKS) load_b(ks + 2, b0);
+        __builtin_amdgcn_sched_barrier(0);
+        kstep(ks + 1, b1);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      // the next row tile's A: in flight behind the stores, waited for at the restage
+      if (restage) load_a(an.p);
+      // C/D layout of 16x16 MFMA: col = lane & 15, row = 4 kq + reg. One base
+      // address per output row (rows past M write the pack's trash line), the
+      // N tiles at immediate offsets; only the last N tile masks columns >= N.
+      float* base[PMT][4];
+#pragma unroll
+      for (int mt = 0; mt < PMT; ++mt) {
+        const longlong2 o01 = *reinterpret_cast<const longlong2*>(orow + 16 * mt + 4 * kq);
+        const longlong2 o23 = *reinterpret_cast<const longlong2*>(orow + 16 * mt + 4 * kq + 2);
+        const int64_t o[4] = {o01.x, o01.y, o23.x, o23.y};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) base[mt][r] = (o[r] >= 0 ? Y + o[r] : trash) + 16 * t0 + lm;
+      }
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        const bool full = 16 * (t0 + j) + 16 <= PN;   // wave-uniform
+#pragma unroll
+        for (int mt = 0; mt < PMT; ++mt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float v = (0.f + acc[mt][j][r]) + bj[j];
+            if (full || 16 * (t0 + j) + lm < PN) base[mt][r][16 * j] = v;
+          }
+      }
+    };
+    switch (live) {
+      case 5: body(std::integral_constant<int, 5>{}); break;
+      case 4: body(std::integral_constant<int, 4>{}); break;
+      default:
+        if (restage) load_a(an.p);   // (no N tiles of its own in this item)
+        break;
+    }
+    if (restage) {
+      __syncthreads();   // every wave is done with this A tile
+      store_a(an.o);
+      __syncthreads();
+    }
+  }
+}
+
+}  // namespace
+
+size_t proj_x6_pack_floats() { return PACK_FLOATS; }
+
+bool proj_x6_supported(int K, int N, const WeightRows& w) {
+  return K == PK && N == PN && w.accumulate == 0 && gemm_arith() != NRMS_GEMM_F32;
+}
+
+int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, hipStream_t s) {
+  if (((uintptr_t)d0 % 16) || (d1 && ((uintptr_t)d1 % 16))) return NRMS_ERR_UNSUPPORTED;
+  constexpr int n = PKS * PNT * 512 + PNT * 16 + 2 * PKP;
+  hipLaunchKernelGGL(proj_x6_pack_kernel, dim3((n + 255) / 256, w1 ? 2 : 1), dim3(256), 0, s, w0,
+                     w1 ? *w1 : w0, d0, d1 ? d1 : d0);
+  return launch_status();
+}
+
+int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
+                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, hipStream_t s) {
+  if (M == 0) return NRMS_OK;
+  if (((uintptr_t)X % 16) || ((uintptr_t)packed % 16) || ar.stride_row % 4 ||
+      (ar.per_batch != INT64_MAX && ar.stride_batch % 4) || ldy < PN)
+    return NRMS_ERR_UNSUPPORTED;
+  if (m_dev && !row_ids) return NRMS_ERR_INVALID_ARG;
+  int dev = 0, n_cu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) n_cu = v;
+  }
+  const int64_t items = (M + PM - 1) / PM * PNR;
+  const int64_t grid = items < n_cu ? items : n_cu;   // persistent: one workgroup per CU
+  if (m_dev) {
+    ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_x6_kernel<true>), (int)P_LDS);
+    hipLaunchKernelGGL(proj_x6_kernel<true>, dim3((unsigned)grid), dim3(256), P_LDS, s, X, n_rows_x, ar, row_ids,
+                       M, packed, Y, ldy, m_dev);
+  } else {
+    ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_x6_kernel<false>), (int)P_LDS);
+    hipLaunchKernelGGL(proj_x6_kernel<false>, dim3((unsigned)grid), dim3(256), P_LDS, s, X, n_rows_x, ar, row_ids,
+                       M, packed, Y, ldy, (const int32_t*)nullptr);
+  }
+  return launch_status();
+}
+
+}  // namespace nrms

@@ -45,7 +45,12 @@ def main():
         st = N.stream_handle(dev)
         P = N.ptr
         wn, wu = ctypes.byref(plan.wn), ctypes.byref(plan.wu)
+        pws = torch.empty(N.load().nrms_qkv_project_workspace_size(D), dtype=torch.uint8, device=dev)
         calls = {
+            "qkv_news_ws": lambda: N.call("nrms_qkv_project_ws", P(plan.table), V, None, V, wn, P(plan.qkv),
+                                          plan.ldq, P(pws), pws.numel(), st),
+            "qkv_user_ws": lambda: N.call("nrms_qkv_project_ws", P(plan.news), n_clk, None, n_clk, wu,
+                                          P(plan.uqkv), plan.uldq, P(pws), pws.numel(), st),
             "qkv_news": lambda: N.call("nrms_qkv_project", P(plan.table), V, None, V, wn, P(plan.qkv),
                                        plan.ldq, st),
             "news_fused": lambda: N.call("nrms_news_attention_pool", P(plan.qkv), plan.ldq, V, P(clk), n_clk,

@@ -378,6 +378,44 @@ def test_stage_abi_matches_module(golden, golden_state, device):
     assert O.normwise_rel_err(_np(qkv), qkv_ref).max() < 1e-5
 
 
+@pytest.mark.parametrize("case", ["table", "table_ld900", "gather_bad_ids", "tiny", "vocab"])
+def test_qkv_project_ws_bitwise_equals_staged_gemm(device, gemm_mode, case):
+    """nrms_qkv_project_ws (W split once per call, A tile resident in LDS:
+    proj_x6.hip) gives bitwise the rows of nrms_qkv_project (the staged GEMM),
+    including NaN rows for invalid ids, row counts off the 64-row tile and the
+    unpadded 900-float stride."""
+    from newsrecommendationsystem_amd import _native as N
+    g = torch.Generator(device="cpu").manual_seed(11)
+    m = _module(W.nrms_state(5, 64), 64, device)
+    w, keep = m.news_encoder.weights()
+    V = {"table": 3013, "table_ld900": 3013, "gather_bad_ids": 500, "tiny": 37, "vocab": 70976}[case]
+    X = (torch.randn(V, 300, generator=g) * 0.5).to(device)
+    ids = None
+    M = V
+    if case == "gather_bad_ids":
+        idt = torch.randint(0, V, (137 * 20,), generator=g)
+        idt[5], idt[77], idt[1000] = -1, V, 0
+        ids = idt.to(device)
+        M = ids.numel()
+    if case == "tiny":
+        M = 5
+    ld = 900 if case == "table_ld900" else N.load().nrms_qkv_row_stride(300)
+    st = N.stream_handle(device)
+    ref = torch.full((M, ld), 7.0, device=device)
+    got = torch.full((M, ld), 7.0, device=device)
+    N.call("nrms_qkv_project", N.ptr(X), V, N.ptr(ids) if ids is not None else None, M, ctypes.byref(w),
+           N.ptr(ref), ld, st)
+    nb = N.load().nrms_qkv_project_workspace_size(300)
+    wsb = torch.empty(nb, dtype=torch.uint8, device=device)
+    N.call("nrms_qkv_project_ws", N.ptr(X), V, N.ptr(ids) if ids is not None else None, M, ctypes.byref(w),
+           N.ptr(got), ld, N.ptr(wsb), nb, st)
+    torch.cuda.synchronize()
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+    if case == "gather_bad_ids":
+        assert torch.isnan(got[[5, 77], :900]).all() and not torch.isnan(got[1000]).any()
+    assert (got[:, 900:] == 7.0).all()   # the row padding is not written
+
+
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("mode", [1, 2])
 def test_plan_matches_forward(device, fused, mode, gemm_mode):
