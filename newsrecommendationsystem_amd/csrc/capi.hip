@@ -120,7 +120,7 @@ int32_t project_qkv(const float* X, int64_t n_rows_x, ARows ar, const int64_t* r
                     hipStream_t s, const int32_t* list_count = nullptr) {
   const int D = w->d_model;
   const WeightRows wr = qkv_rows(w);
-  if (pack && proj_x6_supported(D, 3 * D, wr)) {
+  if (pack && proj_x6_supported(D, 3 * D, wr) && ((uintptr_t)Y % 16) == 0 && ld % 4 == 0) {
     if (!packed)
       if (int32_t st = launch_proj_x6_pack(wr, pack, nullptr, nullptr, s)) return st;
     return launch_proj_x6(X, n_rows_x, ar, row_ids, M, pack, Y, ld, list_count, s);

@@ -37,7 +37,7 @@ constexpr int PMT = PM / 16;                     // 4 M tiles
 constexpr int PTW = 5;                           // N tiles per wave per item
 constexpr int PRANGE = 4 * PTW;                  // N tiles per item
 constexpr int PNR = (PNT + PRANGE - 1) / PRANGE; // items per row tile (3)
-static_assert(PNT - (PNR - 1) * PRANGE >= 16, "every wave of the last range owns 4 or 5 tiles");
+static_assert(PNT > (PNR - 1) * PRANGE, "item ranges");
 // LDS row: [hi 320 | mid 320 | lo 320 | pad 16] bf16 = 1,952 B = 488 dwords
 // (= 40 mod 64): the 16-row x 4-kq fragment reads cover all 64 banks once.
 constexpr int PRB = 3 * PKP + 16;
@@ -45,10 +45,15 @@ constexpr size_t P_LDS = (size_t)PM * PRB * 2 + PM * sizeof(int64_t);
 static_assert(P_LDS <= 160 * 1024, "LDS");
 constexpr int PACK_BF16 = PKS * PNT * 3 * 512;   // B fragments
 constexpr int PTRASH = 16 * PNT;                 // floats: target of the stores of rows past M
+static_assert(PN % 4 == 0, "16-B output pieces");
 // + bias row (0 past N), zero row, NaN row, trash line
-constexpr int PACK_FLOATS = PACK_BF16 / 2 + PNT * 16 + 2 * PKP + PTRASH;
-constexpr int A_F4 = PM * PK / 4;                // float4 pieces of an A tile (4,800)
-constexpr int A_PASSES = (A_F4 + 255) / 256;     // 19 per thread
+#ifdef NRMS_PX_TIMING
+// probe build (profiles/probes/px_phases.py): per-wave phase cycles after the pack
+constexpr int PSTAMP_FLOATS = 256 * 8 * 8 * 2;
+#else
+constexpr int PSTAMP_FLOATS = 0;
+#endif
+constexpr int PACK_FLOATS = PACK_BF16 / 2 + PNT * 16 + 2 * PKP + PTRASH + PSTAMP_FLOATS;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
@@ -99,11 +104,18 @@ __global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, Weight
 // SCATTER: output row m goes to Y row row_ids[m] (row-list mode; the count is
 // *m_dev, written by an earlier launch). Otherwise row_ids (optional) only
 // gathers the A rows (the fused embedding gather of the per-token mode).
-template <bool SCATTER>
-__global__ __launch_bounds__(256, 1) void proj_x6_kernel(const float* __restrict__ X, int64_t n_rows_x, ARows ar,
-                                                        const int64_t* __restrict__ row_ids, int64_t M,
-                                                        const float* __restrict__ packed, float* __restrict__ Y,
-                                                        int64_t ldy, const int32_t* __restrict__ m_dev) {
+// NW waves: 4 (one per SIMD, five N tiles each) or 8 (two per SIMD: waves
+// w < 4 three tiles, w >= 4 two, so each SIMD still owns five tiles of an
+// item and one wave's waits / stores run under its partner's MFMAs).
+template <bool SCATTER, int NW>
+__global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __restrict__ X, int64_t n_rows_x, ARows ar,
+                                                            const int64_t* __restrict__ row_ids, int64_t M,
+                                                            const float* __restrict__ packed, float* __restrict__ Y,
+                                                            int64_t ldy, const int32_t* __restrict__ m_dev) {
+  static_assert(NW == 4 || NW == 8, "waves per workgroup");
+  constexpr int NTH = 64 * NW;
+  constexpr int TPR = NTH / PM;                      // threads per A row (4 or 8)
+  constexpr int AP = (PK / 4 + TPR - 1) / TPR;       // float4 pieces per thread (19 or 10)
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   __bf16* As = reinterpret_cast<__bf16*>(lds_f);
   int64_t* orow = reinterpret_cast<int64_t*>(As + PM * PRB);   // output row offset (-1: no row)
@@ -121,18 +133,18 @@ __global__ __launch_bounds__(256, 1) void proj_x6_kernel(const float* __restrict
   const int lm = lane & 15, kq = lane >> 4;
 
   // K padding: columns 300..319 of every plane stay zero for the whole launch
-  for (int e = tid; e < PM * 3 * ((PKP - PK) / 4); e += 256) {
+  for (int e = tid; e < PM * 3 * ((PKP - PK) / 4); e += NTH) {
     const int r = e / (3 * ((PKP - PK) / 4)), rem = e - r * (3 * ((PKP - PK) / 4));
     const int pl = rem / ((PKP - PK) / 4), c = rem - pl * ((PKP - PK) / 4);
     *reinterpret_cast<uint2*>(As + r * PRB + pl * PKP + PK + 4 * c) = make_uint2(0u, 0u);
   }
 
-  // A tile staging: thread (row ar_ = tid / 4, quarter q = tid % 4) moves the
-  // float4 pieces q, q + 4, .. of one row (19 per thread, the last for q < 3),
-  // from one source pointer per row tile: the row itself, the pack's zero row
-  // (past M) or its NaN row (invalid id: the row becomes NaN, as gemm_x6_kernel)
-  const int ar_ = tid >> 2, aq = tid & 3;
-  const float* zero_row = packed + PACK_FLOATS - PTRASH - 2 * PKP;
+  // A tile staging: thread (row ar_ = tid / TPR, q = tid % TPR) moves the
+  // float4 pieces q, q + TPR, .. of one row, from one source pointer per row
+  // tile: the row itself, the pack's zero row (past M) or its NaN row
+  // (invalid id: the row becomes NaN, as gemm_x6_kernel)
+  const int ar_ = tid / TPR, aq = tid % TPR;
+  const float* zero_row = packed + PACK_FLOATS - PSTAMP_FLOATS - PTRASH - 2 * PKP;
   const float* nan_row = zero_row + PKP;
   struct ASrc {
     const float* p;
@@ -145,18 +157,18 @@ __global__ __launch_bounds__(256, 1) void proj_x6_kernel(const float* __restrict
     const int64_t o = (SCATTER ? id : m) * ldy;
     return ASrc{(uint64_t)id < (uint64_t)n_rows_x ? X + ar.offset(id) : nan_row, o};
   };
-  float4 ra[A_PASSES];
+  float4 ra[AP];
   auto load_a = [&](const float* src) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < A_PASSES; ++j) {
-      const int c4 = aq + 4 * j < PK / 4 ? aq + 4 * j : PK / 4 - 1;   // (the q = 3 lane of the last pass: unused)
+    for (int j = 0; j < AP; ++j) {
+      const int c4 = aq + TPR * j < PK / 4 ? aq + TPR * j : PK / 4 - 1;   // (pieces past the row: unused)
       ra[j] = *reinterpret_cast<const float4*>(src + 4 * c4);
     }
   };
   auto store_a = [&](int64_t o) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < A_PASSES; ++j) {
-      const int c4 = aq + 4 * j;
+    for (int j = 0; j < AP; ++j) {
+      const int c4 = aq + TPR * j;
       if (c4 < PK / 4) {
         uint32_t h0, m0, l0, h1, m1, l1;
         split3x2(ra[j].x, ra[j].y, h0, m0, l0);
@@ -180,111 +192,172 @@ __global__ __launch_bounds__(256, 1) void proj_x6_kernel(const float* __restrict
   const __amdgpu_buffer_rsrc_t brs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(packed), 0, PACK_BF16 * 2, 0x00020000);
   const float* bias = packed + PACK_BF16 / 2;
-  float* trash = const_cast<float*>(packed) + PACK_FLOATS - PTRASH;   // stores of rows past M
+  float* trash = const_cast<float*>(packed) + PACK_FLOATS - PSTAMP_FLOATS - PTRASH;   // stores of rows past M
+#ifdef NRMS_PX_TIMING
+  unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long tprev = __builtin_amdgcn_s_memtime();
+#define NRMS_PX_STAMP(k)                                          \
+  {                                                               \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    tacc[k] += now_ - tprev;                                      \
+    tprev = now_;                                                 \
+  }
+#else
+#define NRMS_PX_STAMP(k)
+#endif
   // A fragments (16x16x32): lane holds A[row lm + 16 mt][32 ks + 8 kq .. + 7] of each plane
   const __bf16* Ab = As + lm * PRB + 8 * kq;
 
-  for (int64_t it = i0; it < i1; ++it) {
-    const int64_t rt = it / PNR;
-    const int rg = (int)(it - rt * PNR);
-    const bool restage = it + 1 < i1 && (it + 1) / PNR != rt;   // workgroup-uniform
-    ASrc an{zero_row, -1};
-    if (restage) an = a_src(rt + 1);   // (its id load completes behind the mainloop)
-    // the range's tiles split evenly over the waves (N = 900: 5/5/5/5, 5/5/5/5, 4/4/4/5)
-    const int r0 = rg * PRANGE, nr = (r0 + PRANGE < PNT ? r0 + PRANGE : PNT) - r0;
-    const int t0 = r0 + w * nr / 4;
-    const int live = r0 + (w + 1) * nr / 4 - t0;
+  // The wave's N tiles of item (row tile rt, range rg): t0 = 20 rg + off ..
+  // t0 + C - 1; tiles past N (the last range has 17) are computed on a clamped
+  // copy and not stored — those waves would otherwise wait at the next restage
+  // barrier for the waves with live tiles.
+  const int off_w = NW == 4 ? PTW * w : (w < 4 ? 3 * w : 12 + 2 * (w - 4));
+  auto run = [&](auto cc) __attribute__((always_inline)) {
+    constexpr int C = decltype(cc)::value;
+    auto tile_of = [&](int64_t item, int j) __attribute__((always_inline)) -> int {
+      const int t = (int)(item % PNR) * PRANGE + off_w + j;
+      return t < PNT ? t : PNT - 1;
+    };
+    // plane-major: the hi planes (first product's B) arrive first
+    auto load_b = [&](int ks, const int (&bvo)[C], bf16x8 (&dst)[C][3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+          dst[j][pl] = __builtin_bit_cast(
+              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(brs, bvo[j], (ks * PNT * 3 + pl) * 1024, 0));
+    };
+    // A fragments of one k-step, lo planes first (the order the products use them)
+    auto load_afrag = [&](int ks, bf16x8 (&a)[PMT][3]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int pl = 2; pl >= 0; --pl)
+#pragma unroll
+        for (int mt = 0; mt < PMT; ++mt)
+          a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * PRB + pl * PKP + 32 * ks);
+    };
+    floatx4 acc[PMT][C];
+    auto kstep = [&](const bf16x8 (&a)[PMT][3], const bf16x8 (&bb)[C][3]) __attribute__((always_inline)) {
+#define NRMS_PX6(PA, PB)                                                                              \
+  _Pragma("unroll") for (int j = 0; j < C; ++j)                                                       \
+  _Pragma("unroll") for (int mt = 0; mt < PMT; ++mt)                                                  \
+      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][PB], a[mt][PA], acc[mt][j], 0, 0, 0);
+      NRMS_PX6(2, 0) NRMS_PX6(1, 1) NRMS_PX6(0, 2) NRMS_PX6(1, 0) NRMS_PX6(0, 1) NRMS_PX6(0, 0)
+#undef NRMS_PX6
+    };
 
-    auto body = [&](auto cc) __attribute__((always_inline)) {
-      constexpr int C = decltype(cc)::value;
-      floatx4 acc[PMT][C];
+    int bvoff[C];
+#pragma unroll
+    for (int j = 0; j < C; ++j) bvoff[j] = lane * 16 + tile_of(i0, j) * 3 * 1024;
+    bf16x8 b0[C][3], b1[C][3];
+    load_b(0, bvoff, b0);   // each item's first k-step is loaded by the previous item
+
+    for (int64_t it = i0; it < i1; ++it) {
+      NRMS_PX_STAMP(0)   // (loop overhead, restage of the previous item)
+      const int64_t rt = it / PNR;
+      const bool restage = it + 1 < i1 && (it + 1) / PNR != rt;   // workgroup-uniform
+      ASrc an{zero_row, -1};
+      if (restage) an = a_src(rt + 1);   // (its id load completes behind the mainloop)
+      const int t0 = (int)(it % PNR) * PRANGE + off_w;
+      float4 bj[C];
+      int bnext[C];
+#pragma unroll
+      for (int j = 0; j < C; ++j) {
+        bj[j] = *reinterpret_cast<const float4*>(bias + 16 * tile_of(it, j) + 4 * kq);   // (0 past N)
+        bnext[j] = lane * 16 + tile_of(it + 1 < i1 ? it + 1 : it, j) * 3 * 1024;
+      }
 #pragma unroll
       for (int mt = 0; mt < PMT; ++mt)
 #pragma unroll
         for (int j = 0; j < C; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-      int bvoff[C];
-      float bj[C];
-#pragma unroll
-      for (int j = 0; j < C; ++j) {
-        bvoff[j] = lane * 16 + (t0 + j) * 3 * 1024;
-        bj[j] = bias[16 * (t0 + j) + lm];   // (0 past N)
-      }
-      // plane-major: the hi planes (first product's B) arrive first
-      auto load_b = [&](int ks, bf16x8 (&dst)[C][3]) __attribute__((always_inline)) {
-#pragma unroll
-        for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-          for (int j = 0; j < C; ++j)
-            dst[j][pl] = __builtin_bit_cast(
-                bf16x8, __builtin_amdgcn_raw_buffer_load_b128(brs, bvoff[j], (ks * PNT * 3 + pl) * 1024, 0));
-      };
-      auto kstep = [&](int ks, const bf16x8 (&bb)[C][3]) __attribute__((always_inline)) {
-        bf16x8 a[PMT][3];
-#pragma unroll
-        for (int pl = 2; pl >= 0; --pl)
-#pragma unroll
-          for (int mt = 0; mt < PMT; ++mt)
-            a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * PRB + pl * PKP + 32 * ks);
-#define NRMS_PX6(PA, PB)                                                                              \
-  _Pragma("unroll") for (int j = 0; j < C; ++j)                                                       \
-  _Pragma("unroll") for (int mt = 0; mt < PMT; ++mt)                                                  \
-      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);
-        NRMS_PX6(2, 0) NRMS_PX6(1, 1) NRMS_PX6(0, 2) NRMS_PX6(1, 0) NRMS_PX6(0, 1) NRMS_PX6(0, 0)
-#undef NRMS_PX6
-      };
-      // two B buffers in turn, each k-step's loads fenced where they are issued
-      bf16x8 b0[C][3], b1[C][3];
-      load_b(0, b0);
+      // two B buffers (and, at one wave per SIMD, two A-fragment buffers) in
+      // turn; each k-step's loads fenced where they are issued (left free, the
+      // scheduler sinks them to their first use); the last k-step pair loads
+      // the next item's first B
+      constexpr bool A2 = NW == 4;
+      bf16x8 a0[PMT][3], a1[PMT][3];
+      if constexpr (A2) load_afrag(0, a0);
 #pragma unroll
       for (int ks = 0; ks < PKS; ks += 2) {
-        load_b(ks + 1, b1);
+        load_b(ks + 1, bvoff, b1);
+        if constexpr (A2) load_afrag(ks + 1, a1);
+        else load_afrag(ks, a0);
         __builtin_amdgcn_sched_barrier(0);
-        kstep(ks, b0);
+        kstep(a0, b0);
         __builtin_amdgcn_sched_barrier(0);
-        if (ks + 2 < PKS) load_b(ks + 2, b0);
-        __builtin_amdgcn_sched_barrier(0);
-        kstep(ks + 1, b1);
+        if (ks == 0) { NRMS_PX_STAMP(1) }   // item setup + first k-step (B(0) / A fragment waits)
+        if (ks + 2 < PKS) {
+          load_b(ks + 2, bvoff, b0);
+          if constexpr (A2) load_afrag(ks + 2, a0);
+        } else if (it + 1 < i1) {
+          load_b(0, bnext, b0);
+        }
+        if constexpr (A2) {
+          __builtin_amdgcn_sched_barrier(0);
+          kstep(a1, b1);
+        } else {
+          load_afrag(ks + 1, a0);
+          __builtin_amdgcn_sched_barrier(0);
+          kstep(a0, b1);
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
+#pragma unroll
+      for (int j = 0; j < C; ++j) bvoff[j] = bnext[j];
+      NRMS_PX_STAMP(2)   // k-steps 1..9
       // the next row tile's A: in flight behind the stores, waited for at the restage
       if (restage) load_a(an.p);
-      // C/D layout of 16x16 MFMA: col = lane & 15, row = 4 kq + reg. One base
-      // address per output row (rows past M write the pack's trash line), the
-      // N tiles at immediate offsets; only the last N tile masks columns >= N.
-      float* base[PMT][4];
+      // The products run with W as the MFMA's A operand, so the 16x16 C/D
+      // layout (col = lane & 15, row = 4 kq + reg) is transposed: lane (lm, kq)
+      // holds output row 16 mt + lm, columns 16 t + 4 kq .. + 3 — one 16-B store
+      // per (M tile, N tile). (Swapping the operands of a product changes no
+      // bit of it; tests compare with gemm_x6_kernel.) One base address per
+      // output row (rows past M write the pack's trash line), the N tiles at
+      // immediate offsets; tiles past N skipped, columns past N of the last masked.
+      float* base[PMT];
 #pragma unroll
       for (int mt = 0; mt < PMT; ++mt) {
-        const longlong2 o01 = *reinterpret_cast<const longlong2*>(orow + 16 * mt + 4 * kq);
-        const longlong2 o23 = *reinterpret_cast<const longlong2*>(orow + 16 * mt + 4 * kq + 2);
-        const int64_t o[4] = {o01.x, o01.y, o23.x, o23.y};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) base[mt][r] = (o[r] >= 0 ? Y + o[r] : trash) + 16 * t0 + lm;
+        const int64_t o = orow[16 * mt + lm];
+        base[mt] = (o >= 0 ? Y + o : trash) + 16 * t0 + 4 * kq;
       }
 #pragma unroll
       for (int j = 0; j < C; ++j) {
-        const bool full = 16 * (t0 + j) + 16 <= PN;   // wave-uniform
+        if (t0 + j >= PNT) break;                         // wave-uniform
+        const bool full = 16 * (t0 + j) + 16 <= PN;       // wave-uniform
 #pragma unroll
-        for (int mt = 0; mt < PMT; ++mt)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float v = (0.f + acc[mt][j][r]) + bj[j];
-            if (full || 16 * (t0 + j) + lm < PN) base[mt][r][16 * j] = v;
-          }
+        for (int mt = 0; mt < PMT; ++mt) {
+          float4 v;
+          v.x = (0.f + acc[mt][j][0]) + bj[j].x;
+          v.y = (0.f + acc[mt][j][1]) + bj[j].y;
+          v.z = (0.f + acc[mt][j][2]) + bj[j].z;
+          v.w = (0.f + acc[mt][j][3]) + bj[j].w;
+#ifdef NRMS_PX_NOSTORE   // probe: the epilogue without its stores
+          if (v.x == 12345.f) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
+#else
+          if (full || 16 * (t0 + j) + 4 * kq < PN) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
+#endif
+        }
       }
-    };
-    switch (live) {
-      case 5: body(std::integral_constant<int, 5>{}); break;
-      case 4: body(std::integral_constant<int, 4>{}); break;
-      default:
-        if (restage) load_a(an.p);   // (no N tiles of its own in this item)
-        break;
+      NRMS_PX_STAMP(3)   // epilogue stores issued
+      if (restage) {
+        __syncthreads();   // every wave is done with this A tile
+        NRMS_PX_STAMP(4)   // barrier wait
+        store_a(an.o);
+        NRMS_PX_STAMP(5)   // A loads landed + split + LDS stores
+        __syncthreads();
+        NRMS_PX_STAMP(6)   // second barrier
+      }
     }
-    if (restage) {
-      __syncthreads();   // every wave is done with this A tile
-      store_a(an.o);
-      __syncthreads();
-    }
+  };
+  if constexpr (NW == 4) run(std::integral_constant<int, PTW>{});
+  else if (w < 4) run(std::integral_constant<int, 3>{});
+  else run(std::integral_constant<int, 2>{});
+#ifdef NRMS_PX_TIMING
+  if (lane == 0) {
+    unsigned long long* dbg = reinterpret_cast<unsigned long long*>(trash + PTRASH);
+    for (int k = 0; k < 8; ++k) dbg[(blockIdx.x * NW + w) * 8 + k] = tacc[k];
   }
+#endif
 }
 
 }  // namespace
@@ -307,7 +380,7 @@ int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t
                        const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, hipStream_t s) {
   if (M == 0) return NRMS_OK;
   if (((uintptr_t)X % 16) || ((uintptr_t)packed % 16) || ar.stride_row % 4 ||
-      (ar.per_batch != INT64_MAX && ar.stride_batch % 4) || ldy < PN)
+      (ar.per_batch != INT64_MAX && ar.stride_batch % 4) || ldy < PN || ((uintptr_t)Y % 16) || ldy % 4)
     return NRMS_ERR_UNSUPPORTED;
   if (m_dev && !row_ids) return NRMS_ERR_INVALID_ARG;
   int dev = 0, n_cu = 256;
@@ -317,14 +390,18 @@ int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t
   }
   const int64_t items = (M + PM - 1) / PM * PNR;
   const int64_t grid = items < n_cu ? items : n_cu;   // persistent: one workgroup per CU
+#ifndef NRMS_PX_WAVES
+#define NRMS_PX_WAVES 8
+#endif
+  constexpr int NW = NRMS_PX_WAVES;
   if (m_dev) {
-    ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_x6_kernel<true>), (int)P_LDS);
-    hipLaunchKernelGGL(proj_x6_kernel<true>, dim3((unsigned)grid), dim3(256), P_LDS, s, X, n_rows_x, ar, row_ids,
-                       M, packed, Y, ldy, m_dev);
+    ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_x6_kernel<true, NW>), (int)P_LDS);
+    hipLaunchKernelGGL((proj_x6_kernel<true, NW>), dim3((unsigned)grid), dim3(64 * NW), P_LDS, s, X, n_rows_x, ar,
+                       row_ids, M, packed, Y, ldy, m_dev);
   } else {
-    ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_x6_kernel<false>), (int)P_LDS);
-    hipLaunchKernelGGL(proj_x6_kernel<false>, dim3((unsigned)grid), dim3(256), P_LDS, s, X, n_rows_x, ar, row_ids,
-                       M, packed, Y, ldy, (const int32_t*)nullptr);
+    ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_x6_kernel<false, NW>), (int)P_LDS);
+    hipLaunchKernelGGL((proj_x6_kernel<false, NW>), dim3((unsigned)grid), dim3(64 * NW), P_LDS, s, X, n_rows_x, ar,
+                       row_ids, M, packed, Y, ldy, (const int32_t*)nullptr);
   }
   return launch_status();
 }
