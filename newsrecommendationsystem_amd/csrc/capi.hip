@@ -134,12 +134,13 @@ int32_t project_qkv(const float* X, int64_t n_rows_x, ARows ar, const int64_t* r
 int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                         int64_t n_seq_a, const int64_t* ids_b, int64_t n_seq, int32_t L,
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
-                        hipStream_t s, float* wap = nullptr, bool* deduped = nullptr) {
+                        hipStream_t s, float* wap = nullptr, bool* deduped = nullptr,
+                        int64_t broadcast_from = 0) {
   const int D = w->d_model;
   if (deduped) *deduped = false;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
     return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
-                             w->q_add, wap, out, s, -1, deduped);
+                             w->q_add, wap, out, s, -1, deduped, broadcast_from);
   if (ldq != 3 * (int64_t)D) return NRMS_ERR_UNSUPPORTED;   // stage kernels: packed rows
   int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
@@ -481,6 +482,12 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
 
   int32_t st;
   bool deduped = false;
+  const int arith = gemm_arith();
+  const bool user_fused = fused_user_supported(N, D, user_w->n_heads, user_w->query_dim) &&
+                          ((uintptr_t)user % 16) == 0;
+  // with the UserEncoder's row-list projection the clicked padding titles'
+  // vectors are never read: only the candidates get the rep group's copies
+  const int64_t bcast_from = (user_fused && arith != NRMS_GEMM_F32) ? n_clk : 0;
   if ((st = rec(0))) return st;
   // both weight sets split once, in one launch
   const WeightRows nwr = qkv_rows(news_w), uwr = qkv_rows(user_w);
@@ -491,7 +498,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
     if (st) return st;
     if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
-                         news, stream, wap, &deduped);
+                         news, stream, wap, &deduped, bcast_from);
   } else {
     st = project_qkv(table, V, contiguous_rows(D), clicked_ids, n_clk * L, news_w, pack, packed, qkv, ld,
                      stream);
@@ -507,13 +514,11 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   if ((st = rec(2))) return st;
   // UserEncoder (src/model/NRMS/user_encoder.py:15-26) over the clicked news
   // vectors. After a deduplicating news launch, the clicked titles of copied
-  // all-padding groups carry bitwise copies of the rep group's vectors, so
-  // their q|k|v rows are the rep rows': only the other rows are projected
-  // (row-list GEMM) and the fused tail reads copied positions from the rep
-  // rows. Bitwise the same logits as projecting every row.
-  const bool user_fused = fused_user_supported(N, D, user_w->n_heads, user_w->query_dim) &&
-                          ((uintptr_t)user % 16) == 0;
-  const bool user_dedupe = deduped && user_fused && gemm_arith() != NRMS_GEMM_F32;
+  // all-padding groups have the rep group's vectors (bitwise; not written out
+  // here, see bcast_from), so their q|k|v rows are the rep rows': only the
+  // other rows are projected (row-list GEMM) and the fused tail reads copied
+  // positions from the rep rows. Bitwise the same logits as projecting every row.
+  const bool user_dedupe = deduped && user_fused && arith != NRMS_GEMM_F32;
   PaddingGroups pg{nullptr, nullptr, nullptr};
   if (user_dedupe) {
     pg = fused_news_padding_groups(wap, n_all);

@@ -261,16 +261,16 @@ __global__ __launch_bounds__(256) void classify_groups_kernel(RowMap rm, int64_t
   if (lead && !pad) list[wbase[w] + __popcll(keep & ((1ull << lane) - 1))] = (int32_t)g;
 }
 
-// out[s] = out[4 rep + s % 4] for every title s of the other all-padding groups.
+// out[s] = out[4 rep + s % 4] for every title s >= s0 of the other all-padding groups.
 __global__ __launch_bounds__(256) void broadcast_padding_kernel(const uint8_t* __restrict__ pad_group,
-                                                                const int32_t* __restrict__ rep,
+                                                                const int32_t* __restrict__ rep, int64_t s0,
                                                                 int64_t n_titles, float* __restrict__ out) {
-  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (title, float4 column)
-  const int64_t s = t / (FD / 4);
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (title - s0, float4 column)
+  const int64_t s = s0 + t / (FD / 4);
   if (s >= n_titles || !pad_group[s / FT]) return;
   const int64_t r = *rep;
   if (s / FT == r) return;
-  const int c = (int)(t - s * (FD / 4));
+  const int c = (int)(t - (s - s0) * (FD / 4));
   reinterpret_cast<float4*>(out + s * FD)[c] =
       reinterpret_cast<const float4*>(out + (r * FT + (s % FT)) * FD)[c];
 }
@@ -947,7 +947,8 @@ unsigned long long* g_fused_dbg = nullptr;   // set by profiles/probes/news_vari
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
-                          float* out, hipStream_t s, int dedupe_setting, bool* deduped) {
+                          float* out, hipStream_t s, int dedupe_setting, bool* deduped,
+                          int64_t broadcast_from) {
   if (deduped) *deduped = false;
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
@@ -1006,10 +1007,13 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes_exact, s, qkv, ldq, rm, gl,
                      ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
-  if (dedupe) {
-    const int64_t nt4 = n_titles * (FD / 4);
+  // (titles below broadcast_from are not copied: nrms_forward's UserEncoder
+  // reads the clicked padding titles from the rep group's rows)
+  const int64_t b0 = broadcast_from < 0 ? 0 : (broadcast_from / FT) * FT;
+  if (dedupe && b0 < n_titles) {
+    const int64_t nt4 = (n_titles - b0) * (FD / 4);
     hipLaunchKernelGGL(broadcast_padding_kernel, dim3((unsigned)((nt4 + 255) / 256)), dim3(256), 0, s,
-                       pad_group, rcount + 2, n_titles, out);
+                       pad_group, rcount + 2, b0, n_titles, out);
   }
   const int32_t st = launch_status();
   if (st == NRMS_OK && deduped) *deduped = dedupe;

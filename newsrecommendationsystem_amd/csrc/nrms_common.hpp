@@ -247,10 +247,13 @@ bool fused_news_supported(int L, int D, int H, int Q);
 // dedupe_setting: -1 = the process-wide nrms_set_title_dedupe setting, else
 // 0 / 1; *deduped (optional) tells whether the padding groups were classified
 // (fused_news_padding_groups is then valid until the workspace is reused).
+// broadcast_from: the copies of the rep group's vectors are written for titles
+// >= broadcast_from (rounded down to a group) only.
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
-                          float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr);
+                          float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr,
+                          int64_t broadcast_from = 0);
 PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles);
 // The rows m < n_rows of titles not copied from rep (the UserEncoder's rows to
 // project), appended to list in any order; their count in *pg.user_count.

@@ -131,6 +131,10 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lm = lane & 15, kq = lane >> 4;
+#ifdef NRMS_PX_STAGGER   // probe: odd workgroups start ~NRMS_PX_STAGGER x 8k cycles late
+  if (blockIdx.x & 1)
+    for (int i = 0; i < NRMS_PX_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
 
   // K padding: columns 300..319 of every plane stay zero for the whole launch
   for (int e = tid; e < PM * 3 * ((PKP - PK) / 4); e += NTH) {
@@ -274,6 +278,52 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
       // turn; each k-step's loads fenced where they are issued (left free, the
       // scheduler sinks them to their first use); the last k-step pair loads
       // the next item's first B
+      // The products run with W as the MFMA's A operand, so the 16x16 C/D
+      // layout (col = lane & 15, row = 4 kq + reg) is transposed: lane (lm, kq)
+      // holds output row 16 mt + lm, columns 16 t + 4 kq .. + 3 — one 16-B store
+      // per (M tile, N tile). (Swapping the operands of a product changes no
+      // bit of it; tests compare with gemm_x6_kernel.) One base address per
+      // output row (rows past M write the pack's trash line), the N tiles at
+      // immediate offsets; tiles past N skipped, columns past N of the last masked.
+      float* base[PMT];
+#pragma unroll
+      for (int mt = 0; mt < PMT; ++mt) {
+        const int64_t o = orow[16 * mt + lm];
+        base[mt] = (o >= 0 ? Y + o : trash) + 16 * t0 + 4 * kq;
+      }
+      auto store_tile = [&](int j) __attribute__((always_inline)) {
+        if (t0 + j >= PNT) return;                        // wave-uniform
+        const bool full = 16 * (t0 + j) + 16 <= PN;       // wave-uniform
+#pragma unroll
+        for (int mt = 0; mt < PMT; ++mt) {
+          float4 v;
+          v.x = (0.f + acc[mt][j][0]) + bj[j].x;
+          v.y = (0.f + acc[mt][j][1]) + bj[j].y;
+          v.z = (0.f + acc[mt][j][2]) + bj[j].z;
+          v.w = (0.f + acc[mt][j][3]) + bj[j].w;
+#ifdef NRMS_PX_NOSTORE   // probe: the epilogue without its stores
+          if (v.x == 12345.f) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
+#else
+          if (full || 16 * (t0 + j) + 4 * kq < PN) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
+#endif
+        }
+      };
+      // the last k-step tile by tile, each tile's stores issued behind the next
+      // tile's MFMAs (the store bursts of all CUs at an item's end cost ~17 % of
+      // the kernel; here they run under the MFMAs)
+      auto kstep_final = [&](const bf16x8 (&a)[PMT][3], const bf16x8 (&bb)[C][3]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < C; ++j) {
+#define NRMS_PX6F(PA, PB)                                                                             \
+  _Pragma("unroll") for (int mt = 0; mt < PMT; ++mt)                                                  \
+      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][PB], a[mt][PA], acc[mt][j], 0, 0, 0);
+          NRMS_PX6F(2, 0) NRMS_PX6F(1, 1) NRMS_PX6F(0, 2) NRMS_PX6F(1, 0) NRMS_PX6F(0, 1) NRMS_PX6F(0, 0)
+#undef NRMS_PX6F
+          if (j > 0) store_tile(j - 1);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        store_tile(C - 1);
+      };
       constexpr bool A2 = NW == 4;
       bf16x8 a0[PMT][3], a1[PMT][3];
       if constexpr (A2) load_afrag(0, a0);
@@ -292,52 +342,22 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
         } else if (it + 1 < i1) {
           load_b(0, bnext, b0);
         }
+        if constexpr (!A2) load_afrag(ks + 1, a0);
+        __builtin_amdgcn_sched_barrier(0);
         if constexpr (A2) {
-          __builtin_amdgcn_sched_barrier(0);
-          kstep(a1, b1);
+          if (ks + 2 < PKS) kstep(a1, b1);
+          else kstep_final(a1, b1);
         } else {
-          load_afrag(ks + 1, a0);
-          __builtin_amdgcn_sched_barrier(0);
-          kstep(a0, b1);
+          if (ks + 2 < PKS) kstep(a0, b1);
+          else kstep_final(a0, b1);
         }
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int j = 0; j < C; ++j) bvoff[j] = bnext[j];
       NRMS_PX_STAMP(2)   // k-steps 1..9
-      // the next row tile's A: in flight behind the stores, waited for at the restage
+      // the next row tile's A: loads in flight until the restage below
       if (restage) load_a(an.p);
-      // The products run with W as the MFMA's A operand, so the 16x16 C/D
-      // layout (col = lane & 15, row = 4 kq + reg) is transposed: lane (lm, kq)
-      // holds output row 16 mt + lm, columns 16 t + 4 kq .. + 3 — one 16-B store
-      // per (M tile, N tile). (Swapping the operands of a product changes no
-      // bit of it; tests compare with gemm_x6_kernel.) One base address per
-      // output row (rows past M write the pack's trash line), the N tiles at
-      // immediate offsets; tiles past N skipped, columns past N of the last masked.
-      float* base[PMT];
-#pragma unroll
-      for (int mt = 0; mt < PMT; ++mt) {
-        const int64_t o = orow[16 * mt + lm];
-        base[mt] = (o >= 0 ? Y + o : trash) + 16 * t0 + 4 * kq;
-      }
-#pragma unroll
-      for (int j = 0; j < C; ++j) {
-        if (t0 + j >= PNT) break;                         // wave-uniform
-        const bool full = 16 * (t0 + j) + 16 <= PN;       // wave-uniform
-#pragma unroll
-        for (int mt = 0; mt < PMT; ++mt) {
-          float4 v;
-          v.x = (0.f + acc[mt][j][0]) + bj[j].x;
-          v.y = (0.f + acc[mt][j][1]) + bj[j].y;
-          v.z = (0.f + acc[mt][j][2]) + bj[j].z;
-          v.w = (0.f + acc[mt][j][3]) + bj[j].w;
-#ifdef NRMS_PX_NOSTORE   // probe: the epilogue without its stores
-          if (v.x == 12345.f) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
-#else
-          if (full || 16 * (t0 + j) + 4 * kq < PN) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
-#endif
-        }
-      }
       NRMS_PX_STAMP(3)   // epilogue stores issued
       if (restage) {
         __syncthreads();   // every wave is done with this A tile

@@ -47,11 +47,13 @@ def main():
         wn, wu = ctypes.byref(plan.wn), ctypes.byref(plan.wu)
         pws = torch.empty(N.load().nrms_qkv_project_workspace_size(D), dtype=torch.uint8, device=dev)
         calls = {
-            "qkv_news_ws": lambda: N.call("nrms_qkv_project_ws", P(plan.table), V, None, V, wn, P(plan.qkv),
-                                          plan.ldq, P(pws), pws.numel(), st),
-            "qkv_user_ws": lambda: N.call("nrms_qkv_project_ws", P(plan.news), n_clk, None, n_clk, wu,
-                                          P(plan.uqkv), plan.uldq, P(pws), pws.numel(), st),
-            "qkv_news": lambda: N.call("nrms_qkv_project", P(plan.table), V, None, V, wn, P(plan.qkv),
+            # the product path's projection (proj_x6.hip, W split once per call)
+            "qkv_news": lambda: N.call("nrms_qkv_project_ws", P(plan.table), V, None, V, wn, P(plan.qkv),
+                                       plan.ldq, P(pws), pws.numel(), st),
+            "qkv_user": lambda: N.call("nrms_qkv_project_ws", P(plan.news), n_clk, None, n_clk, wu,
+                                       P(plan.uqkv), plan.uldq, P(pws), pws.numel(), st),
+            # the staged GEMM (gemm_x6_kernel: nrms_qkv_project)
+            "qkv_news_staged": lambda: N.call("nrms_qkv_project", P(plan.table), V, None, V, wn, P(plan.qkv),
                                        plan.ldq, st),
             "news_fused": lambda: N.call("nrms_news_attention_pool", P(plan.qkv), plan.ldq, V, P(clk), n_clk,
                                          P(cand), n_all, L, wn, P(plan.news), P(plan.fws),
@@ -59,7 +61,7 @@ def main():
             "mhsa_news": lambda: N.call("nrms_self_attention", P(plan.qkv), V, P(clk), n_clk, P(cand), n_all,
                                         L, wn, P(plan.ctx), st),
             "addscore_news": lambda: N.call("nrms_additive_scores", P(plan.ctx), n_all * L, wn, P(plan.scores), st),
-            "qkv_user": lambda: N.call("nrms_qkv_project", P(plan.news), n_clk, None, n_clk, wu, P(plan.uqkv),
+            "qkv_user_staged": lambda: N.call("nrms_qkv_project", P(plan.news), n_clk, None, n_clk, wu, P(plan.uqkv),
                                        plan.uldq, st),
             "mhsa_user": lambda: N.call("nrms_self_attention", P(plan.uqkv), n_clk, None, B, None, B, Nc, wu,
                                         P(plan.uctx), st),

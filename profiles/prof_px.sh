@@ -2,7 +2,7 @@
 # Counter passes of the pre-split-W projection (proj_x6.hip) on the bench's
 # vocabulary GEMM: bash profiles/prof_px.sh <tag> [stage]
 set -euo pipefail
-TAG=${1:-px}; STAGE=${2:-qkv_news_ws}
+TAG=${1:-px}; STAGE=${2:-qkv_news}
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$REPO/gpurun_out/$TAG
 mkdir -p $OUT

@@ -15,8 +15,9 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"news_fused": "fused_news_kernel", "qkv_news": "gemm_x6_kernel",
-           "qkv_user": "gemm_x6_kernel", "user_fused": "fused_user_kernel"}
+KERNELS = {"news_fused": "fused_news_kernel", "qkv_news": "proj_x6_kernel<false",
+           "qkv_user": "proj_x6_kernel", "user_fused": "fused_user_kernel",
+           "qkv_news_staged": "gemm_x6_kernel"}
 
 
 def main():

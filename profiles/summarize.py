@@ -25,6 +25,22 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def stage_of(name, grid_threads, wg):
     """Map (kernel, grid) of the bench workload (B=1024, V=70976) to a stage."""
     blocks = grid_threads // max(wg, 1)
+    if "proj_x6_kernel<true" in name:   # row-list mode: the UserEncoder after dedupe
+        return "qkv_user"
+    if "proj_x6_kernel<false" in name:
+        return "qkv_news"
+    if "proj_x6_pack" in name:
+        return "pack_qkv"
+    if "pack_additive_b" in name:
+        return "pack_add_news"
+    if "pack_user_b" in name:
+        return "pack_add_user"
+    if "classify_groups" in name:
+        return "classify"
+    if "broadcast_padding" in name:
+        return "broadcast"
+    if "user_row_list" in name:
+        return "user_row_list"
     if "gemm_xwt_f32_kernel<12, false>" in name or "gemm_x6" in name:
         return "qkv_user" if blocks in (2000, 4000) else "qkv_news"   # M = 51,200: 128- or 64-row tiles
     if "gemm_xwt_f32_kernel<13" in name:
