@@ -34,6 +34,12 @@ constexpr int UKG = 19;                    // f32 k-groups of 16 (K 300 -> 304)
 constexpr int UNT = 13;                    // N tiles (208 >= 200)
 constexpr int UWAP3 = UKS * UNT * 3 * 64 * 4;   // floats: [ks][nt][plane][lane][8 bf16]
 constexpr int UWAP1 = UKG * UNT * 64 * 4;       // floats: [kg][nt][lane][4]
+constexpr int UWAP_MAX = UWAP3 > UWAP1 ? UWAP3 : UWAP1;
+#ifdef NRMS_USER_TIMING
+constexpr int USTAMP_FLOATS = 4096 * 8 * 2;     // probe: 8 u64 per user (B <= 4096)
+#else
+constexpr int USTAMP_FLOATS = 0;
+#endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void usplit3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
@@ -97,6 +103,17 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   constexpr int NTPW = (UNT + NW - 1) / NW;            // N-tiles per wave
   constexpr int MT = (LMAX + 15) / 16;                 // M-tiles
   extern __shared__ __attribute__((aligned(16))) float ulds[];
+#ifdef NRMS_USER_TIMING   // probe build (profiles/probes/user_phases.py): phase cycles of wave 0
+  unsigned long long ut[8] = {0, 0, 0, 0, 0, 0, 0, 0}, uprev = __builtin_amdgcn_s_memtime();
+#define NRMS_U_STAMP(k)                                           \
+  {                                                               \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime(); \
+    ut[k] = now_ - uprev;                                         \
+    uprev = now_;                                                 \
+  }
+#else
+#define NRMS_U_STAMP(k)
+#endif
   float* tile = ulds;                                  // [LMAX][URS]
   float* part = tile + LMAX * URS;                     // [UNT][64]
   float* wts = part + UNT * 64;                        // [64]
@@ -141,6 +158,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     }
   }
   __syncthreads();
+  NRMS_U_STAMP(0)   // K|V staged
 
   // ---------------- 1. attention: thread = (head, query) ----------------
   float acc[UDK];
@@ -210,6 +228,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     }
   }
   __syncthreads();   // every K|V read done: the tile becomes the context
+  NRMS_U_STAMP(1)   // attention
   if constexpr (MODE == 1) {
     // three bf16 planes per row (plane p at bf16 offset 320 p), k permuted to
     // the MFMA fragment order: lane (lm, kq) of k-step ks reads 16 contiguous
@@ -243,6 +262,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       *reinterpret_cast<float4*>(tile + (e / 5) * URS + UD + 4 * (e % 5)) = make_float4(0.f, 0.f, 0.f, 0.f);
   }
   __syncthreads();
+  NRMS_U_STAMP(2)   // context split + stores
 
   // ---------------- 2. additive GEMM + tanh·q row partials ----------------
   if (w < UNT) {
@@ -330,6 +350,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     }
   }
   __syncthreads();
+  NRMS_U_STAMP(3)   // additive GEMM + tanh·q
 
   // ---------------- 3. softmax over the L rows + pooling ----------------
   if (w == 0) {
@@ -344,6 +365,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     wts[lane] = ex / wave_sum(ex);
   }
   __syncthreads();
+  NRMS_U_STAMP(4)   // softmax
   // two lanes per float4 column (rows of one parity each), 150 lanes in 3 waves
   if (tid < 192) {
     const int u = tid >> 1, par = tid & 1;
@@ -377,6 +399,13 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     o.w += __shfl_xor(o.w, 1);
     if (u < UD / 4 && par == 0) reinterpret_cast<float4*>(out + s * UD)[u] = o;
   }
+#ifdef NRMS_USER_TIMING
+  NRMS_U_STAMP(5)   // pooling
+  if (tid == 0) {
+    unsigned long long* dbg = reinterpret_cast<unsigned long long*>(const_cast<float*>(WaP) + UWAP_MAX);
+    for (int k = 0; k < 8; ++k) dbg[s * 8 + k] = ut[k];
+  }
+#endif
 }
 
 template <int MODE, int LMAX, int NT>
@@ -402,7 +431,7 @@ int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const 
 
 }  // namespace
 
-size_t fused_user_packed_b_floats() { return (size_t)(UWAP3 > UWAP1 ? UWAP3 : UWAP1); }
+size_t fused_user_packed_b_floats() { return (size_t)UWAP_MAX + USTAMP_FLOATS; }
 
 bool fused_user_supported(int L, int D, int H, int Q) {
   return L >= 1 && L <= 64 && D == UD && H == UH && Q == UQ;
