@@ -486,8 +486,9 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   const bool user_fused = fused_user_supported(N, D, user_w->n_heads, user_w->query_dim) &&
                           ((uintptr_t)user % 16) == 0;
   // with the UserEncoder's row-list projection the clicked padding titles'
-  // vectors are never read: only the candidates get the rep group's copies
-  const int64_t bcast_from = (user_fused && arith != NRMS_GEMM_F32) ? n_clk : 0;
+  // vectors are never read, and the scorer reads a copied candidate from the
+  // rep group: no copies are written
+  const int64_t bcast_from = (user_fused && arith != NRMS_GEMM_F32) ? n_all : 0;
   if ((st = rec(0))) return st;
   // both weight sets split once, in one launch
   const WeightRows nwr = qkv_rows(news_w), uwr = qkv_rows(user_w);
@@ -520,6 +521,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   // positions from the rep rows. Bitwise the same logits as projecting every row.
   const bool user_dedupe = deduped && user_fused && arith != NRMS_GEMM_F32;
   PaddingGroups pg{nullptr, nullptr, nullptr};
+  const PaddingGroups pg_all = deduped ? fused_news_padding_groups(wap, n_all) : pg;
   if (user_dedupe) {
     pg = fused_news_padding_groups(wap, n_all);
     if ((st = launch_user_row_list(pg, n_clk, ulist, stream))) return st;
@@ -538,7 +540,8 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
                          stream);
   if (st) return st;
   if ((st = rec(4))) return st;
-  st = launch_score(news + (size_t)n_clk * D, B, C, (int64_t)C * D, D, user, D, D, logits, stream);
+  st = launch_score(news + (size_t)n_clk * D, B, C, (int64_t)C * D, D, user, D, D, logits, stream,
+                    bcast_from == n_all && deduped ? &pg_all : nullptr, n_clk);
   if (st) return st;
   return rec(5);
 }

@@ -264,7 +264,11 @@ int32_t launch_score_pairs(const float* news, int64_t n_news, const float* user,
 int32_t launch_impression_metrics(const float* scores, const int32_t* labels,
                                   const int64_t* offsets, int64_t n_imp, double* out,
                                   hipStream_t s);
+// pg (optional): candidates of copied all-padding groups read the rep group's
+// vector; the candidates are titles title0 + b C + c of a contiguous array
+// (news points at title0's row).
 int32_t launch_score(const float* news, int64_t B, int C, int64_t sb, int64_t sc,
-                     const float* user, int64_t su, int D, float* out, hipStream_t s);
+                     const float* user, int64_t su, int D, float* out, hipStream_t s,
+                     const PaddingGroups* pg = nullptr, int64_t title0 = 0);
 
 }  // namespace nrms
