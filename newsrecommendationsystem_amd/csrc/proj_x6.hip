@@ -339,7 +339,10 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
         if (ks + 2 < PKS) {
           load_b(ks + 2, bvoff, b0);
           if constexpr (A2) load_afrag(ks + 2, a0);
-        } else if (it + 1 < i1) {
+        } else {
+          // unconditional (the last item reloads its own first k-step): behind a
+          // branch, the waitcnt pass merged both paths into vmcnt(0) waits in
+          // the last k-step, i.e. waited for these loads there
           load_b(0, bnext, b0);
         }
         if constexpr (!A2) load_afrag(ks + 1, a0);
