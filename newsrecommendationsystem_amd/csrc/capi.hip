@@ -135,12 +135,12 @@ int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int
                         int64_t n_seq_a, const int64_t* ids_b, int64_t n_seq, int32_t L,
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
                         hipStream_t s, float* wap = nullptr, bool* deduped = nullptr,
-                        int64_t broadcast_from = 0) {
+                        int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0) {
   const int D = w->d_model;
   if (deduped) *deduped = false;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
     return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
-                             w->q_add, wap, out, s, -1, deduped, broadcast_from);
+                             w->q_add, wap, out, s, -1, deduped, broadcast_from, user_list, user_rows);
   if (ldq != 3 * (int64_t)D) return NRMS_ERR_UNSUPPORTED;   // stage kernels: packed rows
   int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
@@ -489,6 +489,8 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   // vectors are never read, and the scorer reads a copied candidate from the
   // rep group: no copies are written
   const int64_t bcast_from = (user_fused && arith != NRMS_GEMM_F32) ? n_all : 0;
+  // ... and the news kernel lists the UserEncoder's rows in its prologue
+  const bool user_rows_here = user_fused && arith != NRMS_GEMM_F32;
   if ((st = rec(0))) return st;
   // both weight sets split once, in one launch
   const WeightRows nwr = qkv_rows(news_w), uwr = qkv_rows(user_w);
@@ -499,7 +501,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
     if (st) return st;
     if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
-                         news, stream, wap, &deduped, bcast_from);
+                         news, stream, wap, &deduped, bcast_from, user_rows_here ? ulist : nullptr, n_clk);
   } else {
     st = project_qkv(table, V, contiguous_rows(D), clicked_ids, n_clk * L, news_w, pack, packed, qkv, ld,
                      stream);
@@ -524,7 +526,8 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   const PaddingGroups pg_all = deduped ? fused_news_padding_groups(wap, n_all) : pg;
   if (user_dedupe) {
     pg = fused_news_padding_groups(wap, n_all);
-    if ((st = launch_user_row_list(pg, n_clk, ulist, stream))) return st;
+    // (listed by the news kernel's prologue in the folded mode; the direct mode
+    // has no ids to deduplicate by, so user_dedupe is false there)
     st = project_qkv(news, n_clk, contiguous_rows(D), ulist, n_clk, user_w, upack, packed, uqkv, uld, stream,
                      pg.user_count);
   } else {

@@ -280,13 +280,14 @@ __global__ __launch_bounds__(256) void broadcast_padding_kernel(const uint8_t* _
 // than rep, whose news vectors are copies of rep's slot m % 4 (the UserEncoder
 // reads those rows from 4 rep + m % 4 instead). Appended in any order (vector
 // atomics, one per wave); the count must start at 0.
-__global__ __launch_bounds__(256) void user_row_list_kernel(const uint8_t* __restrict__ pad_group,
-                                                            const int32_t* __restrict__ rep,
-                                                            int64_t n_rows, int64_t* __restrict__ list,
-                                                            int32_t* __restrict__ count) {
+// One 256-thread block lists rows m0 .. m0 + 255.
+__device__ __forceinline__ void user_row_list_block(const uint8_t* __restrict__ pad_group,
+                                                    const int32_t* __restrict__ rep, int64_t n_rows,
+                                                    int64_t* __restrict__ list, int32_t* __restrict__ count,
+                                                    int64_t m0) {
   // one atomic per block (per-wave atomics on the one counter serialised: 11 us)
   __shared__ int wcount[4], wbase[4];
-  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t m = m0 + threadIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t g = m >> 2;
   const bool keep = m < n_rows && !(pad_group[g] && g != (int64_t)*rep);
@@ -301,6 +302,23 @@ __global__ __launch_bounds__(256) void user_row_list_kernel(const uint8_t* __res
   __syncthreads();
   if (keep) list[wbase[w] + __popcll(ballot & ((1ull << lane) - 1))] = m;
 }
+
+__global__ __launch_bounds__(256) void user_row_list_kernel(const uint8_t* __restrict__ pad_group,
+                                                            const int32_t* __restrict__ rep,
+                                                            int64_t n_rows, int64_t* __restrict__ list,
+                                                            int32_t* __restrict__ count) {
+  user_row_list_block(pad_group, rep, n_rows, list, count, (int64_t)blockIdx.x * 256);
+}
+
+// The UserEncoder's row list, built by the deduplicating main pass itself
+// (nrms_forward): its workgroups list the rows before their first group.
+struct UserRows {
+  int64_t* list;   // null: not built here
+  int64_t n_rows;
+  const uint8_t* pad_group;
+  const int32_t* rep;
+  int32_t* count;
+};
 
 // Rows near fp32 overflow (nrms_common.hpp, kExpRecheck). The main pass
 // (EXACT = false) takes the fast exp everywhere and appends the title groups
@@ -388,11 +406,18 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const float* __restrict__ qkv, int64_t ldq, RowMap rmap, GroupList gl,
     const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
-    RecheckList rl NRMS_TIMING_PARAM) {
+    RecheckList rl, UserRows ur NRMS_TIMING_PARAM) {
   using Off = QkvOffsets;
   constexpr bool X6 = MODE == 1;
   constexpr bool H3 = MODE == 2;
   static_assert(!(H3 && EXACT), "the F16X3 main pass is rechecked by the x6 kernel");
+  if constexpr (!EXACT) {
+    if (ur.list)   // (workgroup-uniform; the padding classification ran in an earlier launch)
+      for (int64_t m0 = (int64_t)blockIdx.x * NTHR; m0 < ur.n_rows; m0 += (int64_t)gridDim.x * NTHR) {
+        user_row_list_block(ur.pad_group, ur.rep, ur.n_rows, ur.list, ur.count, m0);
+        __syncthreads();   // (the block's LDS counters are reused)
+      }
+  }
   extern __shared__ __attribute__((aligned(16))) float lds[];
   float* ctxL = lds;                                   // f32: [80][SC]
   __bf16* ctxB = reinterpret_cast<__bf16*>(lds);       // x6:  [80][XRB] = hi | mid | lo planes
@@ -948,7 +973,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting, bool* deduped,
-                          int64_t broadcast_from) {
+                          int64_t broadcast_from, int64_t* user_list, int64_t user_rows) {
   if (deduped) *deduped = false;
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
@@ -972,6 +997,9 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   // padding-group dedupe needs the token ids (gathered rows), 16-B aligned id rows
   const bool dedupe = dedupe_applies(dedupe_setting < 0 ? title_dedupe() : dedupe_setting, ids_a, ids_b);
   const GroupList gl{dedupe ? glist : nullptr, rcount + 1, rcount + 2};
+  // the UserEncoder's row list (nrms_forward) in the main pass's prologue
+  const UserRows ur{dedupe && user_list && user_rows > 0 ? user_list : nullptr, user_rows, pad_group, rcount + 2,
+                    rcount + 3};
   if (x6) {
     const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
     if (h3)
@@ -1000,12 +1028,12 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
     if (int32_t st = launch_status()) return st;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, gl, ws,
-                     b_add, q_add, out, rl NRMS_TIMING_ARG);
+                     b_add, q_add, out, rl, ur NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
   // the recheck pass: reads the count the main pass left; exits at once when 0
   const int64_t blocks_x = blocks < 64 ? blocks : 64;
   hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes_exact, s, qkv, ldq, rm, gl,
-                     ws, b_add, q_add, out, rl NRMS_TIMING_ARG);
+                     ws, b_add, q_add, out, rl, UserRows{nullptr, 0, nullptr, nullptr, nullptr} NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
   // (titles below broadcast_from are not copied: nrms_forward's UserEncoder
   // reads the clicked padding titles from the rep group's rows)

@@ -248,12 +248,14 @@ bool fused_news_supported(int L, int D, int H, int Q);
 // 0 / 1; *deduped (optional) tells whether the padding groups were classified
 // (fused_news_padding_groups is then valid until the workspace is reused).
 // broadcast_from: the copies of the rep group's vectors are written for titles
-// >= broadcast_from (rounded down to a group) only.
+// >= broadcast_from (rounded down to a group) only. user_list (optional): when
+// the launch deduplicates, the main pass also builds launch_user_row_list's
+// list of titles 0 .. user_rows - 1 (count in the PaddingGroups user_count).
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr,
-                          int64_t broadcast_from = 0);
+                          int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0);
 PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles);
 // The rows m < n_rows of titles not copied from rep (the UserEncoder's rows to
 // project), appended to list in any order; their count in *pg.user_count.
