@@ -135,12 +135,14 @@ int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int
                         int64_t n_seq_a, const int64_t* ids_b, int64_t n_seq, int32_t L,
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
                         hipStream_t s, float* wap = nullptr, bool* deduped = nullptr,
-                        int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0) {
+                        int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0,
+                        bool prepacked = false) {
   const int D = w->d_model;
   if (deduped) *deduped = false;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
     return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
-                             w->q_add, wap, out, s, -1, deduped, broadcast_from, user_list, user_rows);
+                             w->q_add, wap, out, s, -1, deduped, broadcast_from, user_list, user_rows,
+                             prepacked);
   if (ldq != 3 * (int64_t)D) return NRMS_ERR_UNSUPPORTED;   // stage kernels: packed rows
   int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
@@ -492,16 +494,27 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   // ... and the news kernel lists the UserEncoder's rows in its prologue
   const bool user_rows_here = user_fused && arith != NRMS_GEMM_F32;
   if ((st = rec(0))) return st;
-  // both weight sets split once, in one launch
+  // every weight split / packing of the step in one launch: both encoders'
+  // Q|K|V, and (fused tails) both W_add
   const WeightRows nwr = qkv_rows(news_w), uwr = qkv_rows(user_w);
   const bool packed = proj_x6_supported(D, 3 * D, nwr);
-  if (packed && (st = launch_proj_x6_pack(nwr, pack, &uwr, upack, stream))) return st;
+  const bool all_packed = packed && folded && user_fused;   // (the fused news tail takes folded + L = 20)
+  const bool news_fused_ok = fused_news_supported(L, D, news_w->n_heads, news_w->query_dim);
+  if (all_packed && news_fused_ok) {
+    if ((st = launch_forward_pack(nwr, pack, uwr, upack, news_w->w_add, wap, arith == NRMS_GEMM_SPLIT_F16X3,
+                                  user_w->w_add, uwap, stream)))
+      return st;
+  } else if (packed && (st = launch_proj_x6_pack(nwr, pack, &uwr, upack, stream))) {
+    return st;
+  }
+  const bool prepacked = all_packed && news_fused_ok;
   if (folded) {
     st = project_qkv(table, V, contiguous_rows(D), nullptr, V, news_w, pack, packed, qkv, ld, stream);
     if (st) return st;
     if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
-                         news, stream, wap, &deduped, bcast_from, user_rows_here ? ulist : nullptr, n_clk);
+                         news, stream, wap, &deduped, bcast_from, user_rows_here ? ulist : nullptr, n_clk,
+                         prepacked);
   } else {
     st = project_qkv(table, V, contiguous_rows(D), clicked_ids, n_clk * L, news_w, pack, packed, qkv, ld,
                      stream);
@@ -537,7 +550,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   if ((st = rec(3))) return st;
   if (user_fused)
     st = launch_fused_user(uqkv, uld, B, N, user_w->w_add, user_w->b_add, user_w->q_add, uwap, user,
-                           stream, user_dedupe ? &pg : nullptr);
+                           stream, user_dedupe ? &pg : nullptr, prepacked);
   else
     st = encode_from_qkv(uqkv, uld, n_clk, nullptr, B, nullptr, B, N, user_w, uctx, uscores, user,
                          stream);

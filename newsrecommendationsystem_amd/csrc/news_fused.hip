@@ -37,6 +37,7 @@
 // N-tiles 3w..3w+2 for all 5 M-tiles plus (M-tile w, N-tile 12); wave 0 also
 // (M-tile 4, N-tile 12).
 #include "nrms_common.hpp"
+#include "packs.hpp"
 
 #include <atomic>
 #include <cstdlib>
@@ -108,7 +109,7 @@ constexpr int XRH = 2 * XKP + 80;
 constexpr int WAP2_FLOATS = XKS * FNT * 3 * 64 * 4;   // [ks][nt][plane hi' | lo | hi][lane][8 f16]
 constexpr size_t LDS_BYTES_H = (size_t)FROWS * XRH * 2 + (4 * FROWS + 2 * 2 * FROWS) * sizeof(float);
 static_assert(LDS_BYTES_H <= 160 * 1024 && (XRH / 2) % 64 == 40, "f16x3 row stride");
-constexpr float kLoScale = kF16LoScale, kLoUnscale = kF16LoUnscale;
+constexpr float kLoUnscale = kF16LoUnscale;
 typedef nrms_f16x8 f16x8;
 
 __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
@@ -154,34 +155,12 @@ template <bool F16>
 __global__ __launch_bounds__(256) void pack_additive_b3_kernel(const float* __restrict__ Wa,
                                                                float* __restrict__ WaP,
                                                                int32_t* __restrict__ recheck_count) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx < 4) recheck_count[idx] = idx == 2 ? INT32_MAX : 0;
-  constexpr int NE = XKS * FNT * 64 * 8;
-  if (idx >= NE + SPECIAL_FLOATS) return;
-  if (idx >= NE) {
-    const int sidx = idx - NE;
-    WaP[WAP_MAX + sidx] = sidx < ROW ? 0.f : qnan();
-    return;
-  }
-  const int i = idx & 7, lane = (idx >> 3) & 63, nt = (idx >> 9) % FNT, ks = (idx >> 9) / FNT;
-  const int n = 16 * nt + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + i;
-  const float v = (n < FQ && k < FD) ? Wa[n * FD + k] : 0.f;
-  __bf16 hi, mid, lo;
-  split3(v, hi, mid, lo);
-  __bf16* o = reinterpret_cast<__bf16*>(WaP) + (((ks * FNT + nt) * 3) * 64 + lane) * 8 + i;
-  o[0] = hi;
-  o[64 * 8] = mid;
-  o[2 * 64 * 8] = lo;
-  if constexpr (F16) {
-    const _Float16 h = (_Float16)v;
-    _Float16* o2 = reinterpret_cast<_Float16*>(WaP + WAP_MAX + SPECIAL_FLOATS) +
-                   (((ks * FNT + nt) * 3) * 64 + lane) * 8 + i;
-    const float hs = (float)h * kLoScale;   // exact unless it overflows fp16: NaN then (-> recheck)
-    o2[0] = fabsf(hs) < 65504.f ? (_Float16)hs : (_Float16)qnan();
-    o2[64 * 8] = (_Float16)((v - (float)h) * kLoScale);
-    o2[2 * 64 * 8] = h;
-  }
+  pk::pack_news_additive<F16>(blockIdx.x * 256 + threadIdx.x, Wa, WaP, recheck_count);
 }
+static_assert(pk::NEWS_WAP_MAX == WAP_MAX && pk::NEWS_SPECIAL == SPECIAL_FLOATS && pk::KS == XKS &&
+                  pk::NT == FNT && pk::Q == FQ && pk::D == FD && pk::NEWS_X6_ELEMS == XKS * FNT * 64 * 8,
+              "packs.hpp layout");
+static_assert(pk::NEWS_COUNTERS == WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS, "packs.hpp counters");
 
 
 struct RowMap {
@@ -973,7 +952,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting, bool* deduped,
-                          int64_t broadcast_from, int64_t* user_list, int64_t user_rows) {
+                          int64_t broadcast_from, int64_t* user_list, int64_t user_rows, bool prepacked) {
   if (deduped) *deduped = false;
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
@@ -1000,7 +979,9 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   // the UserEncoder's row list (nrms_forward) in the main pass's prologue
   const UserRows ur{dedupe && user_list && user_rows > 0 ? user_list : nullptr, user_rows, pad_group, rcount + 2,
                     rcount + 3};
-  if (x6) {
+  if (prepacked) {
+    // (forward_pack_kernel packed W_add and reset the counters)
+  } else if (x6) {
     const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
     if (h3)
       hipLaunchKernelGGL(pack_additive_b3_kernel<true>, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,

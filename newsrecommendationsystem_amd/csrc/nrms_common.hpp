@@ -182,6 +182,13 @@ bool proj_x6_supported(int K, int N, const WeightRows& w);
 int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, hipStream_t s);
 int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
                        const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, hipStream_t s);
+// nrms_forward's weight packings in one launch (split arithmetic): both
+// encoders' Q|K|V (launch_proj_x6_pack layout), the news W_add into the fused
+// news workspace (f16 planes too when f16x3) with its counters reset, and the
+// UserEncoder W_add (x6 layout) into its workspace.
+int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& wu, float* pu,
+                            const float* news_wadd, float* news_ws, bool news_f16, const float* user_wadd,
+                            float* user_ws, hipStream_t s);
 int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
                                    const float* b, const float* q, int N, float* score,
                                    hipStream_t s);
@@ -234,7 +241,7 @@ bool fused_user_supported(int L, int D, int H, int Q);
 // PaddingGroups) are read from 4 rep + m % 4.
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
-                          hipStream_t s, const PaddingGroups* pg = nullptr);
+                          hipStream_t s, const PaddingGroups* pg = nullptr, bool prepacked = false);
 // Process-wide switch (news_fused.hip): encode one all-padding title per
 // batch and broadcast its vector (nrms_set_title_dedupe; NRMS_DEDUPE=0 in the
 // environment turns it off).
@@ -251,11 +258,14 @@ bool fused_news_supported(int L, int D, int H, int Q);
 // >= broadcast_from (rounded down to a group) only. user_list (optional): when
 // the launch deduplicates, the main pass also builds launch_user_row_list's
 // list of titles 0 .. user_rows - 1 (count in the PaddingGroups user_count).
+// prepacked: ws already holds the packed W_add and reset counters
+// (launch_forward_pack).
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr,
-                          int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0);
+                          int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0,
+                          bool prepacked = false);
 PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles);
 // The rows m < n_rows of titles not copied from rep (the UserEncoder's rows to
 // project), appended to list in any order; their count in *pg.user_count.

@@ -1,0 +1,97 @@
+// Per-element bodies of the W_add packings of the fused news and UserEncoder
+// kernels (layouts documented in news_fused.hip / user_fused.hip), shared so
+// that nrms_forward can pack all of its weights in one launch
+// (proj_x6.hip: forward_pack_kernel). The owning files check that their
+// constants equal these.
+#pragma once
+
+#include "nrms_common.hpp"
+
+namespace nrms {
+namespace pk {
+
+constexpr int D = 300, Q = 200;
+constexpr int KS = 10;                          // bf16 / f16 k-steps of 32 (K 300 -> 320)
+constexpr int NT = 13;                          // N tiles of 16 (208 >= Q)
+constexpr int KG = 19;                          // f32 k-groups of 16 (K 300 -> 304)
+constexpr int ROW = 3 * D;                      // q|k|v row
+// news: [x6 planes | f32 fragments] (max), zero + NaN q|k|v rows, f16 planes
+constexpr int NEWS_WAP_F32 = KG * NT * 64 * 4;
+constexpr int NEWS_WAP_X6 = KS * NT * 3 * 64 * 4;
+constexpr int NEWS_WAP_MAX = NEWS_WAP_X6 > NEWS_WAP_F32 ? NEWS_WAP_X6 : NEWS_WAP_F32;
+constexpr int NEWS_SPECIAL = 2 * ROW;
+constexpr int NEWS_COUNTERS = NEWS_WAP_MAX + NEWS_SPECIAL + NEWS_WAP_X6;   // int32 [4] after the f16 planes
+constexpr int NEWS_X6_ELEMS = KS * NT * 64 * 8;   // threads of the x6 / f16 packing
+constexpr int USER_X6_ELEMS = KS * NT * 64 * 8;
+constexpr int USER_F32_ELEMS = KG * NT * 64 * 4;
+constexpr float kLoScale = kF16LoScale;
+
+__device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
+  hi = (__bf16)x;
+  const float r = x - (float)hi;
+  mid = (__bf16)r;
+  lo = (__bf16)(r - (float)mid);
+}
+
+// News W_add, split arithmetic: element idx < NEWS_X6_ELEMS + NEWS_SPECIAL.
+// x6 planes [ks][nt][plane][lane][8] (bf16 hi | mid | lo of Wa[16 nt + (lane
+// & 15)][32 ks + 8 (lane >> 4) + i], 0 past Q or D); F16: also the fp16 planes
+// (2^11 hi, 2^11-scaled residual, hi) after the special rows; then the zero
+// and NaN q|k|v rows; idx < 4 resets the launch's counters.
+template <bool F16>
+__device__ __forceinline__ void pack_news_additive(int idx, const float* __restrict__ Wa, float* __restrict__ WaP,
+                                                   int32_t* __restrict__ counters) {
+  if (idx < 4) counters[idx] = idx == 2 ? INT32_MAX : 0;
+  if (idx >= NEWS_X6_ELEMS + NEWS_SPECIAL) return;
+  if (idx >= NEWS_X6_ELEMS) {
+    const int sidx = idx - NEWS_X6_ELEMS;
+    WaP[NEWS_WAP_MAX + sidx] = sidx < ROW ? 0.f : qnan();
+    return;
+  }
+  const int i = idx & 7, lane = (idx >> 3) & 63, nt = (idx >> 9) % NT, ks = (idx >> 9) / NT;
+  const int n = 16 * nt + (lane & 15), k = 32 * ks + 8 * (lane >> 4) + i;
+  const float v = (n < Q && k < D) ? Wa[n * D + k] : 0.f;
+  __bf16 hi, mid, lo;
+  split3(v, hi, mid, lo);
+  __bf16* o = reinterpret_cast<__bf16*>(WaP) + (((ks * NT + nt) * 3) * 64 + lane) * 8 + i;
+  o[0] = hi;
+  o[64 * 8] = mid;
+  o[2 * 64 * 8] = lo;
+  if constexpr (F16) {
+    const _Float16 h = (_Float16)v;
+    _Float16* o2 = reinterpret_cast<_Float16*>(WaP + NEWS_WAP_MAX + NEWS_SPECIAL) +
+                   (((ks * NT + nt) * 3) * 64 + lane) * 8 + i;
+    const float hs = (float)h * kLoScale;   // exact unless it overflows fp16: NaN then (-> recheck)
+    o2[0] = fabsf(hs) < 65504.f ? (_Float16)hs : (_Float16)qnan();
+    o2[64 * 8] = (_Float16)((v - (float)h) * kLoScale);
+    o2[2 * 64 * 8] = h;
+  }
+}
+
+// UserEncoder W_add. x6: element idx < USER_X6_ELEMS, element i of lane (n =
+// lane & 15, kq = lane >> 4) is k = 32 ks + 4 kq + (i & 3) + 16 (i >> 2), three
+// bf16 planes. f32: idx < USER_F32_ELEMS, the 16x16x4 layout k = 16 kg + 4 kq + t.
+__device__ __forceinline__ void pack_user_additive(int idx, const float* __restrict__ Wa, float* __restrict__ WaP,
+                                                   int x6) {
+  if (x6) {
+    if (idx >= USER_X6_ELEMS) return;
+    const int i = idx & 7, lane = (idx >> 3) & 63, nt = (idx >> 9) % NT, ks = (idx >> 9) / NT;
+    const int n = 16 * nt + (lane & 15);
+    const int k = 32 * ks + 4 * (lane >> 4) + (i & 3) + 16 * (i >> 2);
+    const float v = (n < Q && k < D) ? Wa[n * D + k] : 0.f;
+    __bf16 hi, mid, lo;
+    split3(v, hi, mid, lo);
+    __bf16* o = reinterpret_cast<__bf16*>(WaP) + (((ks * NT + nt) * 3) * 64 + lane) * 8 + i;
+    o[0] = hi;
+    o[64 * 8] = mid;
+    o[2 * 64 * 8] = lo;
+  } else {
+    if (idx >= USER_F32_ELEMS) return;
+    const int t = idx & 3, lane = (idx >> 2) & 63, nt = (idx >> 8) % NT, c = (idx >> 8) / NT;
+    const int n = 16 * nt + (lane & 15), k = 16 * c + 4 * (lane >> 4) + t;
+    WaP[idx] = (n < Q && k < D) ? Wa[n * D + k] : 0.f;
+  }
+}
+
+}  // namespace pk
+}  // namespace nrms

@@ -22,6 +22,7 @@
 // mid·hi, hi·mid, hi·hi), then (0 + acc) + bias — so the two kernels agree
 // bitwise (tests/test_gpu_parity.py compares them).
 #include "nrms_common.hpp"
+#include "packs.hpp"
 
 #include <type_traits>
 
@@ -66,11 +67,9 @@ __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16&
 // [ks][nt][plane][lane][8]: plane of W[16 nt + (lane & 15)][32 ks + 8 (lane >> 4) + i]
 // (0 past N or K), then bias[16 PNT], a zero row and a NaN row (the A rows of
 // rows past M / of invalid ids). blockIdx.y selects the weight set.
-__global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, WeightRows w1, float* __restrict__ d0,
-                                                           float* __restrict__ d1) {
-  const WeightRows& w = blockIdx.y ? w1 : w0;
-  float* dst = blockIdx.y ? d1 : d0;
-  const int idx = blockIdx.x * 256 + threadIdx.x;
+constexpr int PACK_ELEMS = PKS * PNT * 512 + PNT * 16 + 2 * PKP;   // threads of one weight set's packing
+
+__device__ __forceinline__ void pack_proj(int idx, const WeightRows& w, float* __restrict__ dst) {
   constexpr int NE = PKS * PNT * 512;
   if (idx < NE) {
     const int i = idx & 7, lane = (idx >> 3) & 63, t = idx >> 9;
@@ -99,6 +98,37 @@ __global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, Weight
     const int c = idx - NE - PNT * 16;
     dst[PACK_BF16 / 2 + PNT * 16 + c] = c < PKP ? 0.f : qnan();
   }
+}
+
+__global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, WeightRows w1, float* __restrict__ d0,
+                                                           float* __restrict__ d1) {
+  pack_proj(blockIdx.x * 256 + threadIdx.x, blockIdx.y ? w1 : w0, blockIdx.y ? d1 : d0);
+}
+
+// nrms_forward's four packings in one launch: blocks [0, P) news Q|K|V,
+// [P, 2P) user Q|K|V, then the news W_add (x6 planes, f16 planes if f16, the
+// special rows, the counters), then the UserEncoder W_add (x6 layout).
+constexpr int PACK_BLOCKS = (PACK_ELEMS + 255) / 256;
+constexpr int NEWS_ADD_BLOCKS = (pk::NEWS_X6_ELEMS + pk::NEWS_SPECIAL + 255) / 256;
+constexpr int USER_ADD_BLOCKS = (pk::USER_X6_ELEMS + 255) / 256;
+__global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float* __restrict__ pn, WeightRows wu,
+                                                           float* __restrict__ pu, const float* __restrict__ nwa,
+                                                           float* __restrict__ nws, int nf16,
+                                                           const float* __restrict__ uwa, float* __restrict__ uws) {
+  int b = blockIdx.x;
+  const int t = threadIdx.x;
+  if (b < PACK_BLOCKS) return pack_proj(b * 256 + t, wn, pn);
+  b -= PACK_BLOCKS;
+  if (b < PACK_BLOCKS) return pack_proj(b * 256 + t, wu, pu);
+  b -= PACK_BLOCKS;
+  if (b < NEWS_ADD_BLOCKS) {
+    int32_t* counters = reinterpret_cast<int32_t*>(nws + pk::NEWS_COUNTERS);
+    if (nf16) pk::pack_news_additive<true>(b * 256 + t, nwa, nws, counters);
+    else pk::pack_news_additive<false>(b * 256 + t, nwa, nws, counters);
+    return;
+  }
+  b -= NEWS_ADD_BLOCKS;
+  pk::pack_user_additive(b * 256 + t, uwa, uws, 1);
 }
 
 // SCATTER: output row m goes to Y row row_ids[m] (row-list mode; the count is
@@ -393,9 +423,18 @@ bool proj_x6_supported(int K, int N, const WeightRows& w) {
 
 int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, hipStream_t s) {
   if (((uintptr_t)d0 % 16) || (d1 && ((uintptr_t)d1 % 16))) return NRMS_ERR_UNSUPPORTED;
-  constexpr int n = PKS * PNT * 512 + PNT * 16 + 2 * PKP;
-  hipLaunchKernelGGL(proj_x6_pack_kernel, dim3((n + 255) / 256, w1 ? 2 : 1), dim3(256), 0, s, w0,
-                     w1 ? *w1 : w0, d0, d1 ? d1 : d0);
+  hipLaunchKernelGGL(proj_x6_pack_kernel, dim3(PACK_BLOCKS, w1 ? 2 : 1), dim3(256), 0, s, w0, w1 ? *w1 : w0, d0,
+                     d1 ? d1 : d0);
+  return launch_status();
+}
+
+int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& wu, float* pu,
+                            const float* news_wadd, float* news_ws, bool news_f16, const float* user_wadd,
+                            float* user_ws, hipStream_t s) {
+  if (((uintptr_t)pn | (uintptr_t)pu) % 16) return NRMS_ERR_UNSUPPORTED;
+  const int blocks = 2 * PACK_BLOCKS + NEWS_ADD_BLOCKS + USER_ADD_BLOCKS;
+  hipLaunchKernelGGL(forward_pack_kernel, dim3(blocks), dim3(256), 0, s, wn, pn, wu, pu, news_wadd, news_ws,
+                     news_f16 ? 1 : 0, user_wadd, user_ws);
   return launch_status();
 }
 

@@ -24,6 +24,7 @@
 //   3. softmax over the N rows (max-subtracted, F.softmax) and the pooling
 //      (two lanes per float4 column, combined by a lane shuffle).
 #include "nrms_common.hpp"
+#include "packs.hpp"
 
 namespace nrms {
 namespace {
@@ -42,38 +43,17 @@ constexpr int USTAMP_FLOATS = 0;
 #endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ void usplit3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
-  hi = (__bf16)x;
-  const float r = x - (float)hi;
-  mid = (__bf16)r;
-  lo = (__bf16)(r - (float)mid);
-}
 
 // W_add -> B fragments. x6: element i of lane (n = lane & 15, kq = lane >> 4)
 // is k = 32 ks + 4 kq + (i & 3) + 16 (i >> 2), three bf16 planes. f32: the
 // 16x16x4 layout of the news kernel, k = 16 kg + 4 kq + t.
 __global__ __launch_bounds__(256) void pack_user_b_kernel(const float* __restrict__ Wa,
                                                           float* __restrict__ WaP, int x6) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (x6) {
-    if (idx >= UKS * UNT * 64 * 8) return;
-    const int i = idx & 7, lane = (idx >> 3) & 63, nt = (idx >> 9) % UNT, ks = (idx >> 9) / UNT;
-    const int n = 16 * nt + (lane & 15);
-    const int k = 32 * ks + 4 * (lane >> 4) + (i & 3) + 16 * (i >> 2);
-    const float v = (n < UQ && k < UD) ? Wa[n * UD + k] : 0.f;
-    __bf16 hi, mid, lo;
-    usplit3(v, hi, mid, lo);
-    __bf16* o = reinterpret_cast<__bf16*>(WaP) + (((ks * UNT + nt) * 3) * 64 + lane) * 8 + i;
-    o[0] = hi;
-    o[64 * 8] = mid;
-    o[2 * 64 * 8] = lo;
-  } else {
-    if (idx >= UWAP1) return;
-    const int t = idx & 3, lane = (idx >> 2) & 63, nt = (idx >> 8) % UNT, c = (idx >> 8) / UNT;
-    const int n = 16 * nt + (lane & 15), k = 16 * c + 4 * (lane >> 4) + t;
-    WaP[idx] = (n < UQ && k < UD) ? Wa[n * UD + k] : 0.f;
-  }
+  pk::pack_user_additive(blockIdx.x * 256 + threadIdx.x, Wa, WaP, x6);
 }
+static_assert(pk::KS == UKS && pk::NT == UNT && pk::KG == UKG && pk::Q == UQ && pk::D == UD &&
+                  pk::USER_F32_ELEMS == UWAP1,
+              "packs.hpp layout");
 
 __device__ __forceinline__ float urow16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
@@ -439,7 +419,7 @@ bool fused_user_supported(int L, int D, int H, int Q) {
 
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
-                          hipStream_t s, const PaddingGroups* pgp) {
+                          hipStream_t s, const PaddingGroups* pgp, bool prepacked) {
   const PaddingGroups pg = pgp ? *pgp : PaddingGroups{nullptr, nullptr, nullptr};
   if (B == 0) return NRMS_OK;
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
@@ -447,8 +427,10 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
     return NRMS_ERR_UNSUPPORTED;
   const int x6 = gemm_arith() != NRMS_GEMM_F32 ? 1 : 0;
   const int npk = x6 ? UKS * UNT * 64 * 8 : UWAP1;
-  hipLaunchKernelGGL(pack_user_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap, x6);
-  if (int32_t st = launch_status()) return st;
+  if (!prepacked) {
+    hipLaunchKernelGGL(pack_user_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap, x6);
+    if (int32_t st = launch_status()) return st;
+  }
   if (x6) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
   return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
 }
