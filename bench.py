@@ -280,6 +280,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--unfused", action="store_true", help="separate MHSA / additive / pool kernels")
     ap.add_argument("--no-extras", action="store_true", help="skip the gather / config-2 / direct figures")
+    ap.add_argument("--no-graph", action="store_true", help="time the eager call loop instead of a HIP graph replay")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend for the barrier / max-over-ranks timing (nccl = RCCL); "
                          "gloo lets several ranks share one GPU for a rehearsal")
@@ -356,12 +357,39 @@ def main():
         n_ev = min(steps, 50)
         events = (fwd.make_events(n_ev) if not args.unfused else
                   [[torch.cuda.Event(enable_timing=True) for _ in range(n_st + 1)] for _ in range(n_ev)])
+        # One batch repeated (not --stream): the step is captured once into a
+        # HIP graph (the C ABI is capturable: no allocation, no sync) and
+        # replayed, as a serving loop would; the eager loop is timed beside it.
+        graph = None
+        if not args.unfused and not args.stream and len(full) == 1 and not args.no_graph:
+            side = torch.cuda.Stream(device)
+            side.wait_stream(torch.cuda.current_stream(device))
+            with torch.cuda.stream(side):
+                fwd.run(cand, clk)
+            torch.cuda.current_stream(device).wait_stream(side)
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph):
+                fwd.run(cand, clk)
+            graph.replay()
+            torch.cuda.synchronize()
+            same = same and bool(torch.equal(fwd.logits, y_fwd))
+        eager_ms = None
+        if graph is not None:
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            run_steps(fwd, full, steps)
+            torch.cuda.synchronize()
+            eager_ms = (time.perf_counter() - te) / steps * 1e3
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        run_steps(fwd, full, steps)
+        if graph is not None:
+            for _ in range(steps):
+                graph.replay()
+        else:
+            run_steps(fwd, full, steps)
         if args.stream and tail_fwd is not None and steps == len(full):
             tail_fwd.run(*tail[0])
         torch.cuda.synchronize()
@@ -475,8 +503,13 @@ def main():
                        f"{n_ev} steps after the timed ones (events cost queue time, so the timed steps "
                        f"run without them)",
         "user_rows_projected": n_user,
-        "timed_path": "nrms_forward_timed without events (one C-ABI call per step)" if not args.unfused
+        "timed_path": ("nrms_forward (one C-ABI call) captured once in a HIP graph, replayed per step"
+                       if graph is not None else
+                       "nrms_forward_timed without events (one C-ABI call per step)") if not args.unfused
                       else "ForwardPlan stage kernels (--unfused)",
+        "eager": None if eager_ms is None else {
+            "ms_per_step": round(eager_ms, 4), "impressions_per_s": round(B / (eager_ms / 1e3), 1),
+            "note": "the same call issued from Python every step (no graph)"},
         "forward_paths_bitwise_equal": same,
     }
     if rank == 0 and world == 1 and not args.no_extras and not args.stream:
