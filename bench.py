@@ -370,6 +370,7 @@ def main():
             graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph):
                 fwd.run(cand, clk)
+            fwd.logits.fill_(float("nan"))     # the replay must recompute them
             graph.replay()
             torch.cuda.synchronize()
             same = same and bool(torch.equal(fwd.logits, y_fwd))

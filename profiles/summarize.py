@@ -31,6 +31,8 @@ def stage_of(name, grid_threads, wg):
         return "qkv_news"
     if "proj_x6_pack" in name:
         return "pack_qkv"
+    if "forward_pack" in name:
+        return "pack_all"
     if "pack_additive_b" in name:
         return "pack_add_news"
     if "pack_user_b" in name:

@@ -669,6 +669,45 @@ def test_padding_title_dedupe_is_bitwise_identical(device, pad_frac, gemm_mode):
         assert float((vp - vp[:1]).abs().max()) <= 1e-6 * float(vp.abs().max())
 
 
+def test_forward_graph_replay_recomputes_bitwise(device):
+    """nrms_forward captured in a HIP graph (bench.py's timed step): each
+    replay recomputes the logits from whatever the captured id buffers hold
+    (a new batch copied in gives that batch's eager logits bitwise, logits
+    poisoned between replays come back), with padding titles in the batch so
+    the on-device dedupe classification runs inside the graph."""
+    from newsrecommendationsystem_amd.pipeline import TimedForward
+    V, B = 3000, 64
+    sd = W.nrms_state(93, V)
+    m = _module(sd, V, device)
+    batches = []
+    for seed in (93, 94):
+        cand, clk, _ = W.impressions(seed, 5, B, V)
+        clk = clk.copy()
+        clk[np.random.default_rng(seed).random(clk.shape[:2]) < 0.3] = 0
+        batches.append((torch.from_numpy(cand).to(device), torch.from_numpy(clk).to(device)))
+    fwd = TimedForward(m, B, 5, 50, 20)
+    c, k = batches[0][0].clone(), batches[0][1].clone()
+    with torch.no_grad():
+        eager = [fwd.run(*b).clone() for b in batches]
+        side = torch.cuda.Stream(device)
+        side.wait_stream(torch.cuda.current_stream(device))
+        with torch.cuda.stream(side):
+            fwd.run(c, k)
+        torch.cuda.current_stream(device).wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            fwd.run(c, k)
+        for i in (0, 1, 0):
+            c.copy_(batches[i][0])
+            k.copy_(batches[i][1])
+            fwd.logits.fill_(float("nan"))
+            graph.replay()
+            torch.cuda.synchronize()
+            assert torch.equal(fwd.logits, eager[i]), i
+    assert not torch.equal(eager[0], eager[1])
+    assert torch.isfinite(eager[1]).all()
+
+
 def test_forward_timed_matches_forward_and_records_stages(device):
     """nrms_forward_timed (bench.py's timed step): bitwise the logits of
     nrms_forward / NRMS.forward_ids and of the stage-by-stage ForwardPlan, with
