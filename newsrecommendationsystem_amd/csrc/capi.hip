@@ -113,17 +113,22 @@ size_t news_bytes(const NewsSizes& z) {
 
 // Q|K|V projection of the encoders: the pre-split-W kernel (proj_x6.hip) when
 // the shape and arithmetic allow, packing w into `pack` first unless the
-// caller already did (packed = true); the staged GEMM otherwise. Bitwise the
-// same rows either way. list_count non-null: row-list mode (launch_gemm_store_list).
+// caller already did (packed = true, with the same arith); the staged GEMM
+// otherwise (x6: bitwise the same rows; f16x3: the kernel's scaled split-f16
+// arithmetic, the staged GEMM's x6 rows only within rounding). list_count
+// non-null: row-list mode (launch_gemm_store_list). arith < 0: the current mode.
 int32_t project_qkv(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
                     const nrms_encoder_weights_t* w, float* pack, bool packed, float* Y, int64_t ld,
-                    hipStream_t s, const int32_t* list_count = nullptr) {
+                    hipStream_t s, const int32_t* list_count = nullptr, int arith = -1) {
   const int D = w->d_model;
   const WeightRows wr = qkv_rows(w);
-  if (pack && proj_x6_supported(D, 3 * D, wr) && ((uintptr_t)Y % 16) == 0 && ld % 4 == 0) {
+  if (arith < 0) arith = gemm_arith();
+  const bool h3 = arith == NRMS_GEMM_SPLIT_F16X3;
+  if (pack && arith != NRMS_GEMM_F32 && proj_x6_supported(D, 3 * D, wr) && ((uintptr_t)Y % 16) == 0 &&
+      ld % 4 == 0) {
     if (!packed)
-      if (int32_t st = launch_proj_x6_pack(wr, pack, nullptr, nullptr, s)) return st;
-    return launch_proj_x6(X, n_rows_x, ar, row_ids, M, pack, Y, ld, list_count, s);
+      if (int32_t st = launch_proj_x6_pack(wr, pack, nullptr, nullptr, h3, s)) return st;
+    return launch_proj_x6(X, n_rows_x, ar, row_ids, M, pack, Y, ld, list_count, h3, s);
   }
   if (list_count) return launch_gemm_store_list(X, n_rows_x, row_ids, list_count, M, D, wr, 3 * D, Y, ld, s);
   return launch_gemm_store_rows(X, n_rows_x, ar, row_ids, M, D, wr, 3 * D, Y, ld, s);
@@ -497,19 +502,20 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   // every weight split / packing of the step in one launch: both encoders'
   // Q|K|V, and (fused tails) both W_add
   const WeightRows nwr = qkv_rows(news_w), uwr = qkv_rows(user_w);
-  const bool packed = proj_x6_supported(D, 3 * D, nwr);
+  const bool packed = arith != NRMS_GEMM_F32 && proj_x6_supported(D, 3 * D, nwr);
+  const bool h3 = arith == NRMS_GEMM_SPLIT_F16X3;
   const bool all_packed = packed && folded && user_fused;   // (the fused news tail takes folded + L = 20)
   const bool news_fused_ok = fused_news_supported(L, D, news_w->n_heads, news_w->query_dim);
   if (all_packed && news_fused_ok) {
-    if ((st = launch_forward_pack(nwr, pack, uwr, upack, news_w->w_add, wap, arith == NRMS_GEMM_SPLIT_F16X3,
-                                  user_w->w_add, uwap, stream)))
+    if ((st = launch_forward_pack(nwr, pack, uwr, upack, news_w->w_add, wap, h3, user_w->w_add, uwap, stream)))
       return st;
-  } else if (packed && (st = launch_proj_x6_pack(nwr, pack, &uwr, upack, stream))) {
+  } else if (packed && (st = launch_proj_x6_pack(nwr, pack, &uwr, upack, h3, stream))) {
     return st;
   }
   const bool prepacked = all_packed && news_fused_ok;
   if (folded) {
-    st = project_qkv(table, V, contiguous_rows(D), nullptr, V, news_w, pack, packed, qkv, ld, stream);
+    st = project_qkv(table, V, contiguous_rows(D), nullptr, V, news_w, pack, packed, qkv, ld, stream, nullptr,
+                     arith);
     if (st) return st;
     if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
@@ -517,10 +523,10 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
                          prepacked);
   } else {
     st = project_qkv(table, V, contiguous_rows(D), clicked_ids, n_clk * L, news_w, pack, packed, qkv, ld,
-                     stream);
+                     stream, nullptr, arith);
     if (st) return st;
     st = project_qkv(table, V, contiguous_rows(D), cand_ids, B * C * L, news_w, pack, packed,
-                     qkv + (size_t)n_clk * L * ld, ld, stream);
+                     qkv + (size_t)n_clk * L * ld, ld, stream, nullptr, arith);
     if (st) return st;
     if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, n_all * L, nullptr, n_all, nullptr, n_all, L, news_w, ctx,
@@ -542,9 +548,10 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
     // (listed by the news kernel's prologue in the folded mode; the direct mode
     // has no ids to deduplicate by, so user_dedupe is false there)
     st = project_qkv(news, n_clk, contiguous_rows(D), ulist, n_clk, user_w, upack, packed, uqkv, uld, stream,
-                     pg.user_count);
+                     pg.user_count, arith);
   } else {
-    st = project_qkv(news, n_clk, contiguous_rows(D), nullptr, n_clk, user_w, upack, packed, uqkv, uld, stream);
+    st = project_qkv(news, n_clk, contiguous_rows(D), nullptr, n_clk, user_w, upack, packed, uqkv, uld, stream,
+                     nullptr, arith);
   }
   if (st) return st;
   if ((st = rec(3))) return st;

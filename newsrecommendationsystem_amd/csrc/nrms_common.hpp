@@ -174,20 +174,22 @@ int32_t launch_gemm_store_rows(const float* X, int64_t n_rows_x, ARows ar, const
 // Q|K|V projection with W split once per call (proj_x6.hip): K = 300, N = 900,
 // split arithmetic, no accumulate. The pack (proj_x6_pack_floats() floats,
 // 16-B aligned) is written by launch_proj_x6_pack for one or two weight sets
-// and read by launch_proj_x6; bitwise the result of launch_gemm_store_rows /
-// launch_gemm_store_list. m_dev non-null: row-list mode (row_ids lists the
-// rows, *m_dev their count; outputs written in place).
+// and read by launch_proj_x6 with the same h3. h3 = false: split-bf16 x6,
+// bitwise the result of launch_gemm_store_rows / launch_gemm_store_list;
+// h3 = true: scaled split-f16 x3 (proj_x6.hip). m_dev non-null: row-list mode
+// (row_ids lists the rows, *m_dev their count; outputs written in place).
 size_t proj_x6_pack_floats();
 bool proj_x6_supported(int K, int N, const WeightRows& w);
-int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, hipStream_t s);
+int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, bool h3,
+                            hipStream_t s);
 int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
-                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, hipStream_t s);
+                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, bool h3, hipStream_t s);
 // nrms_forward's weight packings in one launch (split arithmetic): both
-// encoders' Q|K|V (launch_proj_x6_pack layout), the news W_add into the fused
-// news workspace (f16 planes too when f16x3) with its counters reset, and the
-// UserEncoder W_add (x6 layout) into its workspace.
+// encoders' Q|K|V (launch_proj_x6_pack layout, h3 = f16), the news W_add into
+// the fused news workspace (f16 planes too when f16) with its counters reset,
+// and the UserEncoder W_add (x6 layout) into its workspace.
 int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& wu, float* pu,
-                            const float* news_wadd, float* news_ws, bool news_f16, const float* user_wadd,
+                            const float* news_wadd, float* news_ws, bool f16, const float* user_wadd,
                             float* user_ws, hipStream_t s);
 int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
                                    const float* b, const float* q, int N, float* score,

@@ -17,10 +17,25 @@
 //     registers in the unrolled 10-k-step mainloop);
 //   * the next row tile's A rows are loaded into registers during the last
 //     k-step of the tile's last item, split into LDS behind one barrier pair.
-// Each output tile accumulates exactly the MFMA sequence of gemm_x6_kernel —
-// the same k-steps, fragment K order and product order (lo·hi, mid·mid, hi·lo,
-// mid·hi, hi·mid, hi·hi), then (0 + acc) + bias — so the two kernels agree
-// bitwise (tests/test_gpu_parity.py compares them).
+// x6: each output tile accumulates exactly the MFMA sequence of
+// gemm_x6_kernel — the same k-steps, fragment K order and product order
+// (lo·hi, mid·mid, hi·lo, mid·hi, hi·mid, hi·hi), then (0 + acc) + bias — so
+// the two kernels agree bitwise (tests/test_gpu_parity.py compares them).
+//
+// H3 (the default arithmetic, NRMS_GEMM_SPLIT_F16X3): split-f16 with
+// power-of-two scaling, three products instead of six. Every A row and every
+// W row (output column) is scaled by its own power of two, 2^-ea (row max
+// into [2^3, 2^4)) and 2^-ew (into [2^14, 2^15)), which is exact and puts both
+// in fp16's range whatever their magnitude. Then a = hi + 2^-11 lo and
+// w = hi + 2^-11 lo with fp16 hi, lo (11 + 11 significand bits); A also keeps
+// hi' = 2^11 hi (exact, < 2^15), so the products w_lo·a_hi, w_hi·a_lo and
+// w_hi·a_hi' all carry 2^11 and sum in one fp32 accumulator on
+// v_mfma_f32_16x16x32_f16 (fp16 products are exact in fp32), and
+// y = ldexp(acc, ea + ew - 11) + bias. The dropped lo·lo term and the operand
+// residuals are ~2^-22 of each row's / column's largest |value|: the rows stay
+// within fp32 GEMM rounding (tests bound them against an fp64 oracle), with W
+// streamed as two fp16 planes instead of three bf16 planes. A NaN stays NaN;
+// an infinite input gives NaN in its row (column), as x6.
 #include "nrms_common.hpp"
 #include "packs.hpp"
 
@@ -42,7 +57,7 @@ static_assert(PNT > (PNR - 1) * PRANGE, "item ranges");
 // LDS row: [hi 320 | mid 320 | lo 320 | pad 16] bf16 = 1,952 B = 488 dwords
 // (= 40 mod 64): the 16-row x 4-kq fragment reads cover all 64 banks once.
 constexpr int PRB = 3 * PKP + 16;
-constexpr size_t P_LDS = (size_t)PM * PRB * 2 + PM * sizeof(int64_t);
+constexpr size_t P_LDS = (size_t)PM * PRB * 2 + PM * (sizeof(int64_t) + sizeof(int32_t));
 static_assert(P_LDS <= 160 * 1024, "LDS");
 constexpr int PACK_BF16 = PKS * PNT * 3 * 512;   // B fragments
 constexpr int PTRASH = 16 * PNT;                 // floats: target of the stores of rows past M
@@ -54,8 +69,16 @@ constexpr int PSTAMP_FLOATS = 256 * 8 * 8 * 2;
 #else
 constexpr int PSTAMP_FLOATS = 0;
 #endif
-constexpr int PACK_FLOATS = PACK_BF16 / 2 + PNT * 16 + 2 * PKP + PTRASH + PSTAMP_FLOATS;
+// [fragments (x6: 3 bf16 planes, H3: 2 fp16 planes)][bias][zero row][NaN row][trash][H3 column exponents][stamps]
+constexpr int OFF_BIAS = PACK_BF16 / 2, OFF_ZERO = OFF_BIAS + PNT * 16, OFF_NAN = OFF_ZERO + PKP;
+constexpr int OFF_TRASH = OFF_NAN + PKP, OFF_EXP = OFF_TRASH + PTRASH, OFF_STAMP = OFF_EXP + PNT * 16;
+constexpr int PACK_FLOATS = OFF_STAMP + PSTAMP_FLOATS;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr float kTwo11 = 2048.0f;
+
+// unbiased exponent field of |x| (0 -> -127; inf / NaN -> 128)
+__device__ __forceinline__ int exp_field(float ax) { return (int)((__float_as_uint(ax) >> 23) & 255u) - 127; }
 
 __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
   hi = (__bf16)x;
@@ -100,14 +123,58 @@ __device__ __forceinline__ void pack_proj(int idx, const WeightRows& w, float* _
   }
 }
 
+// H3: one wave per W row n < 16 PNT (rows past N: zeros), lane k = lane + 64 i
+// (i < 5 covers the K padding to 320): the row's max |w| (wave reduction)
+// gives its exponent ew; [ks][nt][plane hi | lo][lane][8 f16] as the x6
+// fragments; lane 0 writes the bias and ew. Block PACK_ROWS_H3 / 4 writes the
+// zero and NaN rows.
+constexpr int PACK_BLOCKS_H3 = PNT * 16 / 4 + 1;
+__device__ __forceinline__ void pack_proj_h3(int b, int t, const WeightRows& w, float* __restrict__ dst) {
+  if (b == PACK_BLOCKS_H3 - 1) {
+    for (int c = t; c < 2 * PKP; c += 256) dst[OFF_ZERO + c] = c < PKP ? 0.f : qnan();
+    return;
+  }
+  const int lane = t & 63, n = 4 * b + (t >> 6);
+  const int seg = n < PN ? n / w.seg_rows : 0;
+  const float* wr = w.w[seg] + (int64_t)(n - seg * w.seg_rows) * PK;
+  float v[5], mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int k = lane + 64 * i;
+    v[i] = (n < PN && k < PK) ? wr[k] : 0.f;
+    mx = fmaxf(mx, fabsf(v[i]));
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  const int ew = exp_field(mx) - 14;
+  _Float16* o = reinterpret_cast<_Float16*>(dst);
+  const int nt = n >> 4, r = n & 15;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int k = lane + 64 * i, ks = k >> 5, kq = (k >> 3) & 3;
+    const float x = ldexpf(v[i], -ew);
+    const _Float16 hi = (_Float16)x;
+    const _Float16 lo = (_Float16)((x - (float)hi) * kTwo11);
+    const int e = ((ks * PNT + nt) * 2) * 512 + (r + 16 * kq) * 8 + (k & 7);
+    o[e] = hi;
+    o[e + 512] = lo;
+  }
+  if (lane == 0) {
+    dst[OFF_BIAS + n] = (n < PN && w.b[seg]) ? w.b[seg][n - seg * w.seg_rows] : 0.f;
+    reinterpret_cast<int32_t*>(dst)[OFF_EXP + n] = ew;
+  }
+}
+
 __global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, WeightRows w1, float* __restrict__ d0,
-                                                           float* __restrict__ d1) {
-  pack_proj(blockIdx.x * 256 + threadIdx.x, blockIdx.y ? w1 : w0, blockIdx.y ? d1 : d0);
+                                                           float* __restrict__ d1, int h3) {
+  if (h3) pack_proj_h3(blockIdx.x, threadIdx.x, blockIdx.y ? w1 : w0, blockIdx.y ? d1 : d0);
+  else pack_proj(blockIdx.x * 256 + threadIdx.x, blockIdx.y ? w1 : w0, blockIdx.y ? d1 : d0);
 }
 
 // nrms_forward's four packings in one launch: blocks [0, P) news Q|K|V,
-// [P, 2P) user Q|K|V, then the news W_add (x6 planes, f16 planes if f16, the
-// special rows, the counters), then the UserEncoder W_add (x6 layout).
+// [P, 2P) user Q|K|V (P = PACK_BLOCKS, or PACK_BLOCKS_H3 when f16), then the
+// news W_add (x6 planes, f16 planes if f16, the special rows, the counters),
+// then the UserEncoder W_add (x6 layout).
 constexpr int PACK_BLOCKS = (PACK_ELEMS + 255) / 256;
 constexpr int NEWS_ADD_BLOCKS = (pk::NEWS_X6_ELEMS + pk::NEWS_SPECIAL + 255) / 256;
 constexpr int USER_ADD_BLOCKS = (pk::USER_X6_ELEMS + 255) / 256;
@@ -117,10 +184,17 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
                                                            const float* __restrict__ uwa, float* __restrict__ uws) {
   int b = blockIdx.x;
   const int t = threadIdx.x;
-  if (b < PACK_BLOCKS) return pack_proj(b * 256 + t, wn, pn);
-  b -= PACK_BLOCKS;
-  if (b < PACK_BLOCKS) return pack_proj(b * 256 + t, wu, pu);
-  b -= PACK_BLOCKS;
+  if (nf16) {
+    if (b < PACK_BLOCKS_H3) return pack_proj_h3(b, t, wn, pn);
+    b -= PACK_BLOCKS_H3;
+    if (b < PACK_BLOCKS_H3) return pack_proj_h3(b, t, wu, pu);
+    b -= PACK_BLOCKS_H3;
+  } else {
+    if (b < PACK_BLOCKS) return pack_proj(b * 256 + t, wn, pn);
+    b -= PACK_BLOCKS;
+    if (b < PACK_BLOCKS) return pack_proj(b * 256 + t, wu, pu);
+    b -= PACK_BLOCKS;
+  }
   if (b < NEWS_ADD_BLOCKS) {
     int32_t* counters = reinterpret_cast<int32_t*>(nws + pk::NEWS_COUNTERS);
     if (nf16) pk::pack_news_additive<true>(b * 256 + t, nwa, nws, counters);
@@ -137,8 +211,10 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
 // NW waves: 4 (one per SIMD, five N tiles each) or 8 (two per SIMD: waves
 // w < 4 three tiles, w >= 4 two, so each SIMD still owns five tiles of an
 // item and one wave's waits / stores run under its partner's MFMAs).
-template <bool SCATTER, int NW>
-__global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __restrict__ X, int64_t n_rows_x, ARows ar,
+// H3: the split-f16 arithmetic above (A planes hi | lo | hi' in LDS, W planes
+// hi | lo), else x6.
+template <bool SCATTER, int NW, bool H3>
+__global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __restrict__ X, int64_t n_rows_x, ARows ar,
                                                             const int64_t* __restrict__ row_ids, int64_t M,
                                                             const float* __restrict__ packed, float* __restrict__ Y,
                                                             int64_t ldy, const int32_t* __restrict__ m_dev) {
@@ -146,9 +222,12 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
   constexpr int NTH = 64 * NW;
   constexpr int TPR = NTH / PM;                      // threads per A row (4 or 8)
   constexpr int AP = (PK / 4 + TPR - 1) / TPR;       // float4 pieces per thread (19 or 10)
+  constexpr int NPL = H3 ? 2 : 3;                    // W planes
+  using frag = std::conditional_t<H3, f16x8, bf16x8>;
   extern __shared__ __attribute__((aligned(16))) float lds_f[];
   __bf16* As = reinterpret_cast<__bf16*>(lds_f);
   int64_t* orow = reinterpret_cast<int64_t*>(As + PM * PRB);   // output row offset (-1: no row)
+  int32_t* erow = reinterpret_cast<int32_t*>(orow + PM);       // H3: row exponent ea - 11
 
   if constexpr (SCATTER) {
     const int64_t mc = *m_dev;
@@ -178,8 +257,8 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
   // tile: the row itself, the pack's zero row (past M) or its NaN row
   // (invalid id: the row becomes NaN, as gemm_x6_kernel)
   const int ar_ = tid / TPR, aq = tid % TPR;
-  const float* zero_row = packed + PACK_FLOATS - PSTAMP_FLOATS - PTRASH - 2 * PKP;
-  const float* nan_row = zero_row + PKP;
+  const float* zero_row = packed + OFF_ZERO;
+  const float* nan_row = packed + OFF_NAN;
   struct ASrc {
     const float* p;
     int64_t o;   // output row offset (-1: no row)
@@ -200,6 +279,43 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
     }
   };
   auto store_a = [&](int64_t o) __attribute__((always_inline)) {
+    if constexpr (H3) {
+      // the row's max |a| over its TPR threads (consecutive lanes; pieces past
+      // the row repeat piece 74) -> ea, then a' = 2^-ea a in [2^3, 2^4) at most
+      float mx = 0.f;
+#pragma unroll
+      for (int j = 0; j < AP; ++j)
+        mx = fmaxf(mx, fmaxf(fmaxf(fabsf(ra[j].x), fabsf(ra[j].y)), fmaxf(fabsf(ra[j].z), fabsf(ra[j].w))));
+#pragma unroll
+      for (int d = 1; d < TPR; d <<= 1) mx = fmaxf(mx, __shfl_xor(mx, d));
+      const int ea = exp_field(mx) - 3;
+#pragma unroll
+      for (int j = 0; j < AP; ++j) {
+        const int c4 = aq + TPR * j;
+        if (c4 < PK / 4) {
+          _Float16 h[4], l[4], r[4];
+          const float xs[4] = {ra[j].x, ra[j].y, ra[j].z, ra[j].w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float x = ldexpf(xs[e], -ea);
+            h[e] = (_Float16)x;
+            const float r1 = (x - (float)h[e]) * kTwo11;   // exact
+            l[e] = (_Float16)r1;
+            r[e] = (_Float16)(r1 - (float)l[e]);           // exact (the bits lo misses)
+          }
+          _Float16* d = reinterpret_cast<_Float16*>(As) + ar_ * PRB + 4 * c4;
+          typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+          *reinterpret_cast<f16x4*>(d) = f16x4{h[0], h[1], h[2], h[3]};
+          *reinterpret_cast<f16x4*>(d + PKP) = f16x4{l[0], l[1], l[2], l[3]};
+          *reinterpret_cast<f16x4*>(d + 2 * PKP) = f16x4{r[0], r[1], r[2], r[3]};
+        }
+      }
+      if (aq == 0) {
+        orow[ar_] = o;
+        erow[ar_] = ea - 11;
+      }
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < AP; ++j) {
       const int c4 = aq + TPR * j;
@@ -225,8 +341,9 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
 
   const __amdgpu_buffer_rsrc_t brs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(packed), 0, PACK_BF16 * 2, 0x00020000);
-  const float* bias = packed + PACK_BF16 / 2;
-  float* trash = const_cast<float*>(packed) + PACK_FLOATS - PSTAMP_FLOATS - PTRASH;   // stores of rows past M
+  const float* bias = packed + OFF_BIAS;
+  const int32_t* wexp = reinterpret_cast<const int32_t*>(packed) + OFF_EXP;   // H3 column exponents
+  float* trash = const_cast<float*>(packed) + OFF_TRASH;   // stores of rows past M
 #ifdef NRMS_PX_TIMING
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long tprev = __builtin_amdgcn_s_memtime();
@@ -253,37 +370,78 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
       const int t = (int)(item % PNR) * PRANGE + off_w + j;
       return t < PNT ? t : PNT - 1;
     };
-    // plane-major: the hi planes (first product's B) arrive first
-    auto load_b = [&](int ks, const int (&bvo)[C], bf16x8 (&dst)[C][3]) __attribute__((always_inline)) {
+    // plane-major: x6, the hi planes (first product's B) arrive first; H3,
+    // lo (first product's B) then hi
+    auto load_b = [&](int ks, const int (&bvo)[C], frag (&dst)[C][NPL]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl)
+      for (int q = 0; q < NPL; ++q) {
+        const int pl = H3 ? 1 - q : q;
 #pragma unroll
         for (int j = 0; j < C; ++j)
           dst[j][pl] = __builtin_bit_cast(
-              bf16x8, __builtin_amdgcn_raw_buffer_load_b128(brs, bvo[j], (ks * PNT * 3 + pl) * 1024, 0));
+              frag, __builtin_amdgcn_raw_buffer_load_b128(brs, bvo[j], (ks * PNT * NPL + pl) * 1024, 0));
+      }
     };
-    // A fragments of one k-step, lo planes first (the order the products use them)
-    auto load_afrag = [&](int ks, bf16x8 (&a)[PMT][3]) __attribute__((always_inline)) {
+    // A fragments of one k-step in the order the products use them (x6: lo
+    // planes first; H3: hi, lo, hi')
+    auto load_afrag = [&](int ks, frag (&a)[PMT][3]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int pl = 2; pl >= 0; --pl)
+      for (int q = 0; q < 3; ++q) {
+        const int pl = H3 ? q : 2 - q;
 #pragma unroll
         for (int mt = 0; mt < PMT; ++mt)
-          a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * PRB + pl * PKP + 32 * ks);
+          a[mt][pl] = *reinterpret_cast<const frag*>(Ab + 16 * mt * PRB + pl * PKP + 32 * ks);
+      }
     };
     floatx4 acc[PMT][C];
-    auto kstep = [&](const bf16x8 (&a)[PMT][3], const bf16x8 (&bb)[C][3]) __attribute__((always_inline)) {
-#define NRMS_PX6(PA, PB)                                                                              \
-  _Pragma("unroll") for (int j = 0; j < C; ++j)                                                       \
-  _Pragma("unroll") for (int mt = 0; mt < PMT; ++mt)                                                  \
-      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][PB], a[mt][PA], acc[mt][j], 0, 0, 0);
-      NRMS_PX6(2, 0) NRMS_PX6(1, 1) NRMS_PX6(0, 2) NRMS_PX6(1, 0) NRMS_PX6(0, 1) NRMS_PX6(0, 0)
-#undef NRMS_PX6
+    // one product (A plane PA, W plane PB) of M tile mt, N tile j
+    auto mfma = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL], int mt, int j, int PA, int PB)
+        __attribute__((always_inline)) {
+      if constexpr (H3)
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(bb[j][PB], a[mt][PA], acc[mt][j], 0, 0, 0);
+      else
+        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][PB], a[mt][PA], acc[mt][j], 0, 0, 0);
+    };
+    // H3: 2^11 a = 2^11 hi + lo + r exactly; with w = hi + 2^-11 lo the four
+    // products w_hi·r, w_lo·a_hi, w_hi·a_lo, w_hi·(2^11 a_hi) (formed in
+    // registers, exact) accumulate 2^11 w·a
+    auto mfma_h = [&](const frag& b, const frag& a, int mt, int j) __attribute__((always_inline)) {
+      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc[mt][j], 0, 0, 0);
+    };
+    auto hi_scaled = [&](const frag (&a)[PMT][3], frag (&hs)[PMT]) __attribute__((always_inline)) {
+#pragma unroll
+      for (int mt = 0; mt < PMT; ++mt) hs[mt] = a[mt][0] * (_Float16)kTwo11;
+    };
+    auto kstep = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL]) __attribute__((always_inline)) {
+      if constexpr (H3) {
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+#pragma unroll
+          for (int j = 0; j < C; ++j)
+#pragma unroll
+            for (int mt = 0; mt < PMT; ++mt)
+              mfma_h(bb[j][p == 1 ? 1 : 0], a[mt][p == 0 ? 2 : p == 1 ? 0 : 1], mt, j);
+        frag hs[PMT];
+        hi_scaled(a, hs);
+#pragma unroll
+        for (int j = 0; j < C; ++j)
+#pragma unroll
+          for (int mt = 0; mt < PMT; ++mt) mfma_h(bb[j][0], hs[mt], mt, j);
+      } else {
+        constexpr int pa_[6] = {2, 1, 0, 1, 0, 0}, pb_[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+        for (int p = 0; p < 6; ++p)
+#pragma unroll
+          for (int j = 0; j < C; ++j)
+#pragma unroll
+            for (int mt = 0; mt < PMT; ++mt) mfma(a, bb, mt, j, pa_[p], pb_[p]);
+      }
     };
 
     int bvoff[C];
 #pragma unroll
-    for (int j = 0; j < C; ++j) bvoff[j] = lane * 16 + tile_of(i0, j) * 3 * 1024;
-    bf16x8 b0[C][3], b1[C][3];
+    for (int j = 0; j < C; ++j) bvoff[j] = lane * 16 + tile_of(i0, j) * NPL * 1024;
+    frag b0[C][NPL], b1[C][NPL];
     load_b(0, bvoff, b0);   // each item's first k-step is loaded by the previous item
 
     for (int64_t it = i0; it < i1; ++it) {
@@ -294,11 +452,13 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
       if (restage) an = a_src(rt + 1);   // (its id load completes behind the mainloop)
       const int t0 = (int)(it % PNR) * PRANGE + off_w;
       float4 bj[C];
+      int4 ej[C];   // H3: column exponents
       int bnext[C];
 #pragma unroll
       for (int j = 0; j < C; ++j) {
         bj[j] = *reinterpret_cast<const float4*>(bias + 16 * tile_of(it, j) + 4 * kq);   // (0 past N)
-        bnext[j] = lane * 16 + tile_of(it + 1 < i1 ? it + 1 : it, j) * 3 * 1024;
+        if constexpr (H3) ej[j] = *reinterpret_cast<const int4*>(wexp + 16 * tile_of(it, j) + 4 * kq);
+        bnext[j] = lane * 16 + tile_of(it + 1 < i1 ? it + 1 : it, j) * NPL * 1024;
       }
 #pragma unroll
       for (int mt = 0; mt < PMT; ++mt)
@@ -316,10 +476,12 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
       // output row (rows past M write the pack's trash line), the N tiles at
       // immediate offsets; tiles past N skipped, columns past N of the last masked.
       float* base[PMT];
+      int ea[PMT];   // H3: row exponent - 11
 #pragma unroll
       for (int mt = 0; mt < PMT; ++mt) {
         const int64_t o = orow[16 * mt + lm];
         base[mt] = (o >= 0 ? Y + o : trash) + 16 * t0 + 4 * kq;
+        if constexpr (H3) ea[mt] = erow[16 * mt + lm];
       }
       auto store_tile = [&](int j) __attribute__((always_inline)) {
         if (t0 + j >= PNT) return;                        // wave-uniform
@@ -327,10 +489,17 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
 #pragma unroll
         for (int mt = 0; mt < PMT; ++mt) {
           float4 v;
-          v.x = (0.f + acc[mt][j][0]) + bj[j].x;
-          v.y = (0.f + acc[mt][j][1]) + bj[j].y;
-          v.z = (0.f + acc[mt][j][2]) + bj[j].z;
-          v.w = (0.f + acc[mt][j][3]) + bj[j].w;
+          if constexpr (H3) {
+            v.x = ldexpf(acc[mt][j][0], ea[mt] + ej[j].x) + bj[j].x;
+            v.y = ldexpf(acc[mt][j][1], ea[mt] + ej[j].y) + bj[j].y;
+            v.z = ldexpf(acc[mt][j][2], ea[mt] + ej[j].z) + bj[j].z;
+            v.w = ldexpf(acc[mt][j][3], ea[mt] + ej[j].w) + bj[j].w;
+          } else {
+            v.x = (0.f + acc[mt][j][0]) + bj[j].x;
+            v.y = (0.f + acc[mt][j][1]) + bj[j].y;
+            v.z = (0.f + acc[mt][j][2]) + bj[j].z;
+            v.w = (0.f + acc[mt][j][3]) + bj[j].w;
+          }
 #ifdef NRMS_PX_NOSTORE   // probe: the epilogue without its stores
           if (v.x == 12345.f) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
 #else
@@ -341,21 +510,31 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
       // the last k-step tile by tile, each tile's stores issued behind the next
       // tile's MFMAs (the store bursts of all CUs at an item's end cost ~17 % of
       // the kernel; here they run under the MFMAs)
-      auto kstep_final = [&](const bf16x8 (&a)[PMT][3], const bf16x8 (&bb)[C][3]) __attribute__((always_inline)) {
+      auto kstep_final = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL]) __attribute__((always_inline)) {
+        [[maybe_unused]] frag hs[PMT];
+        if constexpr (H3) hi_scaled(a, hs);
 #pragma unroll
         for (int j = 0; j < C; ++j) {
-#define NRMS_PX6F(PA, PB)                                                                             \
-  _Pragma("unroll") for (int mt = 0; mt < PMT; ++mt)                                                  \
-      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][PB], a[mt][PA], acc[mt][j], 0, 0, 0);
-          NRMS_PX6F(2, 0) NRMS_PX6F(1, 1) NRMS_PX6F(0, 2) NRMS_PX6F(1, 0) NRMS_PX6F(0, 1) NRMS_PX6F(0, 0)
-#undef NRMS_PX6F
+          if constexpr (H3) {
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+              for (int mt = 0; mt < PMT; ++mt)
+                mfma_h(bb[j][p == 1 ? 1 : 0], p == 3 ? hs[mt] : a[mt][p == 0 ? 2 : p == 1 ? 0 : 1], mt, j);
+          } else {
+            constexpr int pa_[6] = {2, 1, 0, 1, 0, 0}, pb_[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+            for (int p = 0; p < 6; ++p)
+#pragma unroll
+              for (int mt = 0; mt < PMT; ++mt) mfma(a, bb, mt, j, pa_[p], pb_[p]);
+          }
           if (j > 0) store_tile(j - 1);
           __builtin_amdgcn_sched_barrier(0);
         }
         store_tile(C - 1);
       };
       constexpr bool A2 = NW == 4;
-      bf16x8 a0[PMT][3], a1[PMT][3];
+      frag a0[PMT][3], a1[PMT][3];
       if constexpr (A2) load_afrag(0, a0);
 #pragma unroll
       for (int ks = 0; ks < PKS; ks += 2) {
@@ -407,7 +586,7 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_x6_kernel(const float* __rest
   else run(std::integral_constant<int, 2>{});
 #ifdef NRMS_PX_TIMING
   if (lane == 0) {
-    unsigned long long* dbg = reinterpret_cast<unsigned long long*>(trash + PTRASH);
+    unsigned long long* dbg = reinterpret_cast<unsigned long long*>(const_cast<float*>(packed) + OFF_STAMP);
     for (int k = 0; k < 8; ++k) dbg[(blockIdx.x * NW + w) * 8 + k] = tacc[k];
   }
 #endif
@@ -421,25 +600,40 @@ bool proj_x6_supported(int K, int N, const WeightRows& w) {
   return K == PK && N == PN && w.accumulate == 0 && gemm_arith() != NRMS_GEMM_F32;
 }
 
-int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, hipStream_t s) {
+int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, bool h3,
+                            hipStream_t s) {
   if (((uintptr_t)d0 % 16) || (d1 && ((uintptr_t)d1 % 16))) return NRMS_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(proj_x6_pack_kernel, dim3(PACK_BLOCKS, w1 ? 2 : 1), dim3(256), 0, s, w0, w1 ? *w1 : w0, d0,
-                     d1 ? d1 : d0);
+  hipLaunchKernelGGL(proj_x6_pack_kernel, dim3(h3 ? PACK_BLOCKS_H3 : PACK_BLOCKS, w1 ? 2 : 1), dim3(256), 0, s, w0,
+                     w1 ? *w1 : w0, d0, d1 ? d1 : d0, h3 ? 1 : 0);
   return launch_status();
 }
 
 int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& wu, float* pu,
-                            const float* news_wadd, float* news_ws, bool news_f16, const float* user_wadd,
+                            const float* news_wadd, float* news_ws, bool f16, const float* user_wadd,
                             float* user_ws, hipStream_t s) {
   if (((uintptr_t)pn | (uintptr_t)pu) % 16) return NRMS_ERR_UNSUPPORTED;
-  const int blocks = 2 * PACK_BLOCKS + NEWS_ADD_BLOCKS + USER_ADD_BLOCKS;
+  const int blocks = 2 * (f16 ? PACK_BLOCKS_H3 : PACK_BLOCKS) + NEWS_ADD_BLOCKS + USER_ADD_BLOCKS;
   hipLaunchKernelGGL(forward_pack_kernel, dim3(blocks), dim3(256), 0, s, wn, pn, wu, pu, news_wadd, news_ws,
-                     news_f16 ? 1 : 0, user_wadd, user_ws);
+                     f16 ? 1 : 0, user_wadd, user_ws);
   return launch_status();
 }
 
+namespace {
+template <bool SCATTER, bool H3>
+void launch_proj_kernel(int64_t grid, const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
+                        const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, hipStream_t s) {
+#ifndef NRMS_PX_WAVES
+#define NRMS_PX_WAVES 8
+#endif
+  constexpr int NW = NRMS_PX_WAVES;
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_qkv_kernel<SCATTER, NW, H3>), (int)P_LDS);
+  hipLaunchKernelGGL((proj_qkv_kernel<SCATTER, NW, H3>), dim3((unsigned)grid), dim3(64 * NW), P_LDS, s, X, n_rows_x,
+                     ar, row_ids, M, packed, Y, ldy, m_dev);
+}
+}  // namespace
+
 int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
-                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, hipStream_t s) {
+                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, bool h3, hipStream_t s) {
   if (M == 0) return NRMS_OK;
   if (((uintptr_t)X % 16) || ((uintptr_t)packed % 16) || ar.stride_row % 4 ||
       (ar.per_batch != INT64_MAX && ar.stride_batch % 4) || ldy < PN || ((uintptr_t)Y % 16) || ldy % 4)
@@ -452,18 +646,12 @@ int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t
   }
   const int64_t items = (M + PM - 1) / PM * PNR;
   const int64_t grid = items < n_cu ? items : n_cu;   // persistent: one workgroup per CU
-#ifndef NRMS_PX_WAVES
-#define NRMS_PX_WAVES 8
-#endif
-  constexpr int NW = NRMS_PX_WAVES;
   if (m_dev) {
-    ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_x6_kernel<true, NW>), (int)P_LDS);
-    hipLaunchKernelGGL((proj_x6_kernel<true, NW>), dim3((unsigned)grid), dim3(64 * NW), P_LDS, s, X, n_rows_x, ar,
-                       row_ids, M, packed, Y, ldy, m_dev);
+    if (h3) launch_proj_kernel<true, true>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, m_dev, s);
+    else launch_proj_kernel<true, false>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, m_dev, s);
   } else {
-    ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_x6_kernel<false, NW>), (int)P_LDS);
-    hipLaunchKernelGGL((proj_x6_kernel<false, NW>), dim3((unsigned)grid), dim3(64 * NW), P_LDS, s, X, n_rows_x, ar,
-                       row_ids, M, packed, Y, ldy, (const int32_t*)nullptr);
+    if (h3) launch_proj_kernel<false, true>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, nullptr, s);
+    else launch_proj_kernel<false, false>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, nullptr, s);
   }
   return launch_status();
 }

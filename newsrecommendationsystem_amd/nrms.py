@@ -124,7 +124,7 @@ class NewsEncoder(nn.Module):
         ps = [self.word_embedding.weight] + [
             getattr(getattr(self.multihead_self_attention, n), a)
             for n in ("W_Q", "W_K", "W_V") for a in ("weight", "bias")]
-        return tuple((p.data_ptr(), p._version) for p in ps)
+        return tuple((p.data_ptr(), p._version) for p in ps) + (N.load().nrms_get_gemm_arith(),)
 
     def folded_table(self):
         """Projected vocabulary [V, 3D] (E [W_Q;W_K;W_V]^T + b), cached while
@@ -137,7 +137,9 @@ class NewsEncoder(nn.Module):
         w, keep = self.weights()
         ld = N.load().nrms_qkv_row_stride(D)   # rows padded to whole 128-B lines
         qkv = torch.empty(V, ld, dtype=torch.float32, device=tab.device)
-        N.call("nrms_qkv_project", N.ptr(tab), V, None, V, ctypes_byref(w), N.ptr(qkv), ld,
+        nb = N.load().nrms_qkv_project_workspace_size(D)   # the pre-split-W projection, as nrms_forward's
+        ws = torch.empty(nb, dtype=torch.uint8, device=tab.device)
+        N.call("nrms_qkv_project_ws", N.ptr(tab), V, None, V, ctypes_byref(w), N.ptr(qkv), ld, N.ptr(ws), nb,
                N.stream_handle(tab.device))
         self._folded = (key, qkv)
         return qkv

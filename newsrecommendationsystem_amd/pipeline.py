@@ -55,6 +55,9 @@ class ForwardPlan:
         self.uscores = torch.empty(B * n_clicked, **f32)
         self.user = torch.empty(B, D, **f32)
         self.logits = torch.empty(B, C, **f32)
+        # the projections run through nrms_qkv_project_ws (W split once per
+        # call), as nrms_forward's: the same rows under every arithmetic
+        self.pws = torch.empty(lib.nrms_qkv_project_workspace_size(D), dtype=torch.uint8, device=self.dev)
         self.wn, self._keep_n = ne.weights()
         self.wu, self._keep_u = model.user_encoder.weights()
         self.fused = fused
@@ -82,14 +85,15 @@ class ForwardPlan:
 
         rec(0)
         ldq, uldq = self.ldq, self.uldq
+        pws, npws = P(self.pws), self.pws.numel()
         if self.folded:
-            N.call("nrms_qkv_project", P(self.table), V, None, V, wn, P(self.qkv), ldq, st)
+            N.call("nrms_qkv_project_ws", P(self.table), V, None, V, wn, P(self.qkv), ldq, pws, npws, st)
         else:
-            N.call("nrms_qkv_project", P(self.table), V, P(clicked_ids), n_clk * L, wn,
-                   P(self.qkv), ldq, st)
+            N.call("nrms_qkv_project_ws", P(self.table), V, P(clicked_ids), n_clk * L, wn,
+                   P(self.qkv), ldq, pws, npws, st)
             tail = self.qkv[n_clk * L:]
-            N.call("nrms_qkv_project", P(self.table), V, P(cand_ids), B * C * L, wn, P(tail), ldq,
-                   st)
+            N.call("nrms_qkv_project_ws", P(self.table), V, P(cand_ids), B * C * L, wn, P(tail), ldq,
+                   pws, npws, st)
         rec(1)
         k = 1
         rows, ia, ib = (V, P(clicked_ids), P(cand_ids)) if self.folded else (n_all * L, None, None)
@@ -106,7 +110,7 @@ class ForwardPlan:
             k += 2
         k += 1
         rec(k)
-        N.call("nrms_qkv_project", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), uldq, st)
+        N.call("nrms_qkv_project_ws", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), uldq, pws, npws, st)
         rec(k + 1)
         if self.user_fused:
             N.call("nrms_user_attention_pool", P(self.uqkv), uldq, B, Nc, wu, P(self.user),

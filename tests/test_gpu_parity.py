@@ -339,7 +339,14 @@ def test_full_size_properties(device, gemm_mode):
 
 
 def test_stage_abi_matches_module(golden, golden_state, device):
-    """The per-stage entry points compose to the same news vectors."""
+    """The per-stage entry points compose to the same news vectors (split-bf16
+    x6: the staged projection and the module's pre-split one agree bitwise)."""
+    from newsrecommendationsystem_amd import _native as N
+    with N.gemm_arith(N.NRMS_GEMM_SPLIT_BF16X6):
+        _stage_abi_matches_module(golden, golden_state, device)
+
+
+def _stage_abi_matches_module(golden, golden_state, device):
     from newsrecommendationsystem_amd import _native as N
     m = _module(golden_state, int(golden["V"]), device, hip_cache_folded_table=False,
                 hip_proj_mode=1)
@@ -379,11 +386,13 @@ def test_stage_abi_matches_module(golden, golden_state, device):
 
 
 @pytest.mark.parametrize("case", ["table", "table_ld900", "gather_bad_ids", "tiny", "vocab"])
-def test_qkv_project_ws_bitwise_equals_staged_gemm(device, gemm_mode, case):
+def test_qkv_project_ws_vs_staged_gemm(device, gemm_mode, case):
     """nrms_qkv_project_ws (W split once per call, A tile resident in LDS:
-    proj_x6.hip) gives bitwise the rows of nrms_qkv_project (the staged GEMM),
-    including NaN rows for invalid ids, row counts off the 64-row tile and the
-    unpadded 900-float stride."""
+    proj_x6.hip) against nrms_qkv_project (the staged GEMM): bitwise the same
+    rows under x6 (and f32, where both are the staged GEMM); under f16x3 (the
+    kernel's scaled split-f16 arithmetic) within 2e-6 of the fp64 oracle per
+    row, as the staged rows. NaN rows for invalid ids, row counts off the
+    64-row tile, the unpadded 900-float stride."""
     from newsrecommendationsystem_amd import _native as N
     g = torch.Generator(device="cpu").manual_seed(11)
     m = _module(W.nrms_state(5, 64), 64, device)
@@ -410,10 +419,60 @@ def test_qkv_project_ws_bitwise_equals_staged_gemm(device, gemm_mode, case):
     N.call("nrms_qkv_project_ws", N.ptr(X), V, N.ptr(ids) if ids is not None else None, M, ctypes.byref(w),
            N.ptr(got), ld, N.ptr(wsb), nb, st)
     torch.cuda.synchronize()
-    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+    if gemm_mode != "f16x3":
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+    else:
+        xa = X.cpu().numpy().astype(np.float64)
+        ia = np.arange(M) if ids is None else ids.cpu().numpy()
+        ok = (ia >= 0) & (ia < V)
+        sd = W.nrms_state(5, 64)
+        p = "news_encoder.multihead_self_attention"
+        want = np.concatenate([O.linear(xa[ia[ok]], sd[f"{p}.{n_}.weight"], sd[f"{p}.{n_}.bias"], np.float64)
+                               for n_ in ("W_Q", "W_K", "W_V")], axis=1)
+        g_ok, r_ok = _np(got[:, :900])[ok], _np(ref[:, :900])[ok]
+        assert O.normwise_rel_err(g_ok, want).max() < 2e-6
+        assert O.normwise_rel_err(r_ok, want).max() < 2e-6
+        assert torch.isnan(got[torch.from_numpy(~ok).to(device), :900]).all()
     if case == "gather_bad_ids":
         assert torch.isnan(got[[5, 77], :900]).all() and not torch.isnan(got[1000]).any()
     assert (got[:, 900:] == 7.0).all()   # the row padding is not written
+
+
+def test_qkv_project_f16x3_range(device):
+    """The f16x3 projection's power-of-two scaling (proj_x6.hip): A rows from
+    1e-20 to 1e30 in magnitude (beyond fp16's range both ways) against W_Q
+    scaled by 1e5 and W_K by 1e-8 project within 2e-6 of the fp64 oracle per
+    row and per Q / K / V segment; an all-zero row gives exactly the bias, a
+    row holding an inf gives NaN."""
+    from newsrecommendationsystem_amd import _native as N
+    sd = dict(W.nrms_state(5, 64))
+    p = "news_encoder.multihead_self_attention"
+    sd[f"{p}.W_Q.weight"] = (sd[f"{p}.W_Q.weight"] * np.float32(1e5)).astype(np.float32)
+    sd[f"{p}.W_K.weight"] = (sd[f"{p}.W_K.weight"] * np.float32(1e-8)).astype(np.float32)
+    m = _module(sd, 64, device)
+    w, keep = m.news_encoder.weights()
+    rng = np.random.default_rng(3)
+    M = 300
+    xs = rng.standard_normal((M, 300)) * 10.0 ** rng.uniform(-20, 30, (M, 1))
+    xs[7] = 0.0
+    xs[11, 5] = np.inf
+    X = torch.from_numpy(xs.astype(np.float32)).to(device)
+    got = torch.empty(M, 900, device=device)
+    nb = N.load().nrms_qkv_project_workspace_size(300)
+    wsb = torch.empty(nb, dtype=torch.uint8, device=device)
+    with N.gemm_arith(N.NRMS_GEMM_SPLIT_F16X3):
+        N.call("nrms_qkv_project_ws", N.ptr(X), M, None, M, ctypes.byref(w), N.ptr(got), 0, N.ptr(wsb), nb,
+               N.stream_handle(device))
+    torch.cuda.synchronize()
+    g = _np(got)
+    xa = X.cpu().numpy().astype(np.float64)
+    fine = np.ones(M, bool)
+    fine[[7, 11]] = False
+    for i, n_ in enumerate(("W_Q", "W_K", "W_V")):
+        want = O.linear(xa[fine], sd[f"{p}.{n_}.weight"], sd[f"{p}.{n_}.bias"], np.float64)
+        assert O.normwise_rel_err(g[fine, 300 * i:300 * (i + 1)], want).max() < 2e-6, n_
+        assert np.array_equal(g[7, 300 * i:300 * (i + 1)], sd[f"{p}.{n_}.bias"])
+    assert np.isnan(g[11]).all()
 
 
 @pytest.mark.parametrize("fused", [True, False])
@@ -552,8 +611,10 @@ def test_fused_user_tail_vs_stages(device, B, n_clk, gemm_mode):
     st = N.stream_handle(device)
     lib = N.load()
     uqkv = torch.empty(B * n_clk, 900, device=device)
-    N.call("nrms_qkv_project", N.ptr(x), B * n_clk, None, B * n_clk, ctypes.byref(w), N.ptr(uqkv), 0,
-           st)
+    pb = lib.nrms_qkv_project_workspace_size(300)
+    pws = torch.empty(pb, dtype=torch.uint8, device=device)
+    N.call("nrms_qkv_project_ws", N.ptr(x), B * n_clk, None, B * n_clk, ctypes.byref(w), N.ptr(uqkv), 0,
+           N.ptr(pws), pb, st)
     out = torch.empty(B, 300, device=device)
     nb = lib.nrms_user_attention_pool_workspace_size(B, n_clk, 300)
     ws = torch.empty(nb, dtype=torch.uint8, device=device)
