@@ -23,19 +23,23 @@
 // the two kernels agree bitwise (tests/test_gpu_parity.py compares them).
 //
 // H3 (the default arithmetic, NRMS_GEMM_SPLIT_F16X3): split-f16 with
-// power-of-two scaling, three products instead of six. Every A row and every
+// power-of-two scaling, four products instead of six. Every A row and every
 // W row (output column) is scaled by its own power of two, 2^-ea (row max
 // into [2^3, 2^4)) and 2^-ew (into [2^14, 2^15)), which is exact and puts both
-// in fp16's range whatever their magnitude. Then a = hi + 2^-11 lo and
-// w = hi + 2^-11 lo with fp16 hi, lo (11 + 11 significand bits); A also keeps
-// hi' = 2^11 hi (exact, < 2^15), so the products w_lo·a_hi, w_hi·a_lo and
-// w_hi·a_hi' all carry 2^11 and sum in one fp32 accumulator on
+// in fp16's range whatever their magnitude. A is split into three fp16
+// pieces, 2^11 a = 2^11 hi + lo + r exactly (hi = fp16(a), lo = fp16 of the
+// 2^11-scaled residual, r the bits lo misses); W into two, w = hi + 2^-11 lo
+// (22 bits). The products w_hi·r, w_lo·a_hi, w_hi·a_lo and w_hi·(2^11 a_hi)
+// (formed in registers) all carry 2^11 and sum in one fp32 accumulator on
 // v_mfma_f32_16x16x32_f16 (fp16 products are exact in fp32), and
-// y = ldexp(acc, ea + ew - 11) + bias. The dropped lo·lo term and the operand
-// residuals are ~2^-22 of each row's / column's largest |value|: the rows stay
-// within fp32 GEMM rounding (tests bound them against an fp64 oracle), with W
-// streamed as two fp16 planes instead of three bf16 planes. A NaN stays NaN;
-// an infinite input gives NaN in its row (column), as x6.
+// y = ldexp(acc, ea + ew - 11) + bias. The dropped terms (w_lo·(lo + r),
+// W's residual) are ~2^-22 of each column's largest |w|: the rows stay within
+// fp32 GEMM rounding (tests bound them against an fp64 oracle), and a W that
+// fits in 11 bits (e.g. the overflow-boundary fixtures' one-hot W_Q) gives
+// products as exact as fp32's — the reference's raw-exp overflow boundary is
+// reproduced. W streams as two fp16 planes instead of three bf16 planes. A
+// NaN stays NaN; an infinite input gives NaN in its row (column), as x6.
+
 #include "nrms_common.hpp"
 #include "packs.hpp"
 
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
 // NW waves: 4 (one per SIMD, five N tiles each) or 8 (two per SIMD: waves
 // w < 4 three tiles, w >= 4 two, so each SIMD still owns five tiles of an
 // item and one wave's waits / stores run under its partner's MFMAs).
-// H3: the split-f16 arithmetic above (A planes hi | lo | hi' in LDS, W planes
+// H3: the split-f16 arithmetic above (A planes hi | lo | r in LDS, W planes
 // hi | lo), else x6.
 template <bool SCATTER, int NW, bool H3>
 __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __restrict__ X, int64_t n_rows_x, ARows ar,
