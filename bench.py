@@ -285,7 +285,7 @@ def main():
                     help="process-group backend for the barrier / max-over-ranks timing (nccl = RCCL); "
                          "gloo lets several ranks share one GPU for a rehearsal")
     ap.add_argument("--gemm", choices=["f16x3", "x6", "f32"], default="f16x3",
-                    help="GEMM arithmetic: split-f16 x3 additive GEMM + split-bf16 x6 projections "
+                    help="GEMM arithmetic: split-f16 news additive GEMM and Q|K|V projections "
                          "(default), split-bf16 x6 everywhere, or exact f32 MFMA (all fp32-accurate)")
     args = ap.parse_args()
 
@@ -482,8 +482,9 @@ def main():
         "dtype": {"f32": "fp32",
                   "x6": "fp32 (GEMMs: exact 3-way bf16 split, 6 products, fp32 accumulate)",
                   "f16x3": "fp32 (additive GEMM: 2-plane fp16 split, 22-bit operands, 3 products, fp32 "
-                           "accumulate, out-of-fp16-range groups recomputed x6; projections: 3-way bf16 "
-                           "split, 6 products)"}[args.gemm],
+                           "accumulate, out-of-fp16-range groups recomputed x6; Q|K|V projections: "
+                           "power-of-two-scaled fp16 split, A exact in 3 pieces, W 22-bit, 4 products, fp32 "
+                           "accumulate; UserEncoder additive GEMM: 3-way bf16 split, 6 products)"}[args.gemm],
         "data": "synthetic (MIND-shaped stream: counter-hash ids, random-init weights, N(0,1) embedding table)",
         "config": {"workload": workload, "global_batch": B * world,
                    "impressions_per_gpu": B, "candidates": C, "clicked": N_CLICKED,

@@ -90,13 +90,19 @@ typedef enum { NRMS_PROJ_AUTO = 0, NRMS_PROJ_DIRECT = 1, NRMS_PROJ_FOLDED = 2 } 
  * mode's) at 6/16 of the f32-MFMA cycles.
  * SPLIT_F16X3 (default): the news encoder's additive projection splits each
  * operand into two fp16 planes, a = hi + 2^-11 lo (22 significand bits), and
- * accumulates hi·hi and hi·lo + lo·hi in two fp32 accumulators on
+ * accumulates lo·hi + hi·lo + hi·(2^11 hi) in one fp32 accumulator on
  * v_mfma_f32_16x16x32_f16 (3 products instead of 6); the dropped terms are
  * ~2^-22 |a||b|, normwise error vs fp64 still below a plain fp32 GEMM's. An
  * operand outside fp16's range (|a| >= 65,520) turns its outputs into NaN,
  * and those title groups are recomputed by the SPLIT_BF16X6 / reference-exp
- * recheck pass, so results never depend on the range. The other GEMMs run
- * SPLIT_BF16X6 in this mode.
+ * recheck pass, so results never depend on the range. The encoders' Q|K|V
+ * projections (nrms_qkv_project_ws, nrms_forward, the encode entry points)
+ * scale every input row and every weight row by a power of two into fp16's
+ * range (exact, any magnitude), split the input exactly into three fp16
+ * pieces and the weights into two (22 bits), and accumulate four products:
+ * fp32-GEMM accuracy, and products as exact as fp32's for weights that fit
+ * in 11 bits. The staged nrms_qkv_project and the UserEncoder's additive GEMM
+ * run SPLIT_BF16X6 in this mode.
  * F32: v_mfma_f32_16x16x4_f32, each product an exact fp32 FMA.
  * Process-wide; the initial value comes from the environment (NRMS_GEMM=f32
  * selects F32, NRMS_GEMM=x6 SPLIT_BF16X6). Returns the previous mode, or

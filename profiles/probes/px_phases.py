@@ -1,4 +1,4 @@
-"""Phase cycles of proj_x6_kernel (s_memtime stamps, probe build):
+"""Phase cycles of proj_qkv_kernel (s_memtime stamps, probe build):
     bash _ab/build_variant.sh pxt proj_x6.hip -DNRMS_PX_TIMING
     NRMS_LIB_PATH=_ab/lib_pxt.so python profiles/probes/px_phases.py
 Runs the bench's vocabulary projection (V = 70,976 rows) through

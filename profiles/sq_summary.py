@@ -15,8 +15,8 @@ import os
 import sys
 from collections import defaultdict
 
-KERNELS = {"news_fused": "fused_news_kernel", "qkv_news": "proj_x6_kernel<false",
-           "qkv_user": "proj_x6_kernel", "user_fused": "fused_user_kernel",
+KERNELS = {"news_fused": "fused_news_kernel", "qkv_news": "proj_qkv_kernel<false",
+           "qkv_user": "proj_qkv_kernel", "user_fused": "fused_user_kernel",
            "qkv_news_staged": "gemm_x6_kernel"}
 
 

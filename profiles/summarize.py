@@ -25,9 +25,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 def stage_of(name, grid_threads, wg):
     """Map (kernel, grid) of the bench workload (B=1024, V=70976) to a stage."""
     blocks = grid_threads // max(wg, 1)
-    if "proj_x6_kernel<true" in name:   # row-list mode: the UserEncoder after dedupe
+    if "proj_x6_kernel<true" in name or "proj_qkv_kernel<true" in name:   # row-list mode: the UserEncoder after dedupe
         return "qkv_user"
-    if "proj_x6_kernel<false" in name:
+    if "proj_x6_kernel<false" in name or "proj_qkv_kernel<false" in name:
         return "qkv_news"
     if "proj_x6_pack" in name:
         return "pack_qkv"
