@@ -93,5 +93,44 @@ __device__ __forceinline__ void pack_user_additive(int idx, const float* __restr
   }
 }
 
+// UserEncoder W_add, split-f16 (user_fused.hip MODE 2): one wave per W row
+// n < 16 NT (block b holds rows 4b..4b+3; rows past Q are zeros), lane k =
+// lane + 64 i (i < 5 covers the K padding to 320). The row's max |w| gives its
+// exponent ew (into [2^14, 2^15)); planes hi | lo (w' = hi + 2^-11 lo) in the
+// x6 fragment layout [ks][nt][plane][lane][8] with two planes, k of element i
+// of lane (n & 15) + 16 kq = 32 ks + 4 kq + (i & 3) + 16 (i >> 2); ew as int32
+// at float offset USER_H3_EXP.
+constexpr int USER_H3_BLOCKS = NT * 16 / 4;
+constexpr int USER_H3_EXP = KS * NT * 2 * 64 * 4;
+__device__ __forceinline__ int exp_field(float ax) { return (int)((__float_as_uint(ax) >> 23) & 255u) - 127; }
+__device__ __forceinline__ void pack_user_additive_h3(int b, int t, const float* __restrict__ Wa,
+                                                      float* __restrict__ WaP) {
+  const int lane = t & 63, n = 4 * b + (t >> 6);
+  float v[5], mx = 0.f;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int k = lane + 64 * i;
+    v[i] = (n < Q && k < D) ? Wa[n * D + k] : 0.f;
+    mx = fmaxf(mx, fabsf(v[i]));
+  }
+#pragma unroll
+  for (int o = 32; o; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  const int ew = exp_field(mx) - 14;
+  _Float16* o = reinterpret_cast<_Float16*>(WaP);
+  const int nt = n >> 4;
+#pragma unroll
+  for (int i = 0; i < 5; ++i) {
+    const int k = lane + 64 * i, ks = k >> 5, wi = k & 31, rem = wi & 15;
+    const int kq = rem >> 2, e = 4 * (wi >> 4) + (rem & 3);
+    const float x = ldexpf(v[i], -ew);
+    const _Float16 hi = (_Float16)x;
+    const _Float16 lo = (_Float16)((x - (float)hi) * kF16LoScale);
+    const int off = ((ks * NT + nt) * 2) * 512 + ((n & 15) + 16 * kq) * 8 + e;
+    o[off] = hi;
+    o[off + 512] = lo;
+  }
+  if (lane == 0) reinterpret_cast<int32_t*>(WaP)[USER_H3_EXP + n] = ew;
+}
+
 }  // namespace pk
 }  // namespace nrms

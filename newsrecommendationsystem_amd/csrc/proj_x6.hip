@@ -82,7 +82,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 constexpr float kTwo11 = 2048.0f;
 
 // unbiased exponent field of |x| (0 -> -127; inf / NaN -> 128)
-__device__ __forceinline__ int exp_field(float ax) { return (int)((__float_as_uint(ax) >> 23) & 255u) - 127; }
+using pk::exp_field;
 
 __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16& lo) {
   hi = (__bf16)x;
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, Weight
 // nrms_forward's four packings in one launch: blocks [0, P) news Q|K|V,
 // [P, 2P) user Q|K|V (P = PACK_BLOCKS, or PACK_BLOCKS_H3 when f16), then the
 // news W_add (x6 planes, f16 planes if f16, the special rows, the counters),
-// then the UserEncoder W_add (x6 layout).
+// then the UserEncoder W_add (x6 layout, or split-f16 when f16).
 constexpr int PACK_BLOCKS = (PACK_ELEMS + 255) / 256;
 constexpr int NEWS_ADD_BLOCKS = (pk::NEWS_X6_ELEMS + pk::NEWS_SPECIAL + 255) / 256;
 constexpr int USER_ADD_BLOCKS = (pk::USER_X6_ELEMS + 255) / 256;
@@ -206,7 +206,8 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
     return;
   }
   b -= NEWS_ADD_BLOCKS;
-  pk::pack_user_additive(b * 256 + t, uwa, uws, 1);
+  if (nf16) pk::pack_user_additive_h3(b, t, uwa, uws);
+  else pk::pack_user_additive(b * 256 + t, uwa, uws, 1);
 }
 
 // SCATTER: output row m goes to Y row row_ids[m] (row-list mode; the count is
@@ -616,7 +617,8 @@ int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& w
                             const float* news_wadd, float* news_ws, bool f16, const float* user_wadd,
                             float* user_ws, hipStream_t s) {
   if (((uintptr_t)pn | (uintptr_t)pu) % 16) return NRMS_ERR_UNSUPPORTED;
-  const int blocks = 2 * (f16 ? PACK_BLOCKS_H3 : PACK_BLOCKS) + NEWS_ADD_BLOCKS + USER_ADD_BLOCKS;
+  const int blocks = 2 * (f16 ? PACK_BLOCKS_H3 : PACK_BLOCKS) + NEWS_ADD_BLOCKS +
+                     (f16 ? pk::USER_H3_BLOCKS : USER_ADD_BLOCKS);
   hipLaunchKernelGGL(forward_pack_kernel, dim3(blocks), dim3(256), 0, s, wn, pn, wu, pu, news_wadd, news_ws,
                      f16 ? 1 : 0, user_wadd, user_ws);
   return launch_status();

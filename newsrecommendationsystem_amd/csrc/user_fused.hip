@@ -23,6 +23,16 @@
 //      per-row partials of q_n tanh(y + b_n), one LDS row per N-tile;
 //   3. softmax over the N rows (max-subtracted, F.softmax) and the pooling
 //      (two lanes per float4 column, combined by a lane shuffle).
+// MODE 2 (split-f16, the default arithmetic): each context row is scaled by
+// a power of two, 2^-ea (its max |value| into [2^3, 2^4), from an LDS
+// atomic max over the row's 15 head threads), and stored as three fp16
+// planes, 2^11 a' = 2^11 hi + lo + r (exact for every value within 2^-15 of
+// the row max; the pooling rebuilds the context from them); W_add comes split
+// per output column (packs.hpp pack_user_additive_h3). The GEMM reads two
+// planes and accumulates a_hi·w_lo + a_lo·w_hi + (2^11 a_hi)·w_hi on
+// v_mfma_f32_16x16x32_f16 (three products instead of six, 22-bit operands as
+// the news kernel's additive GEMM), y = ldexp(acc, ea + ew - 11). No range
+// fallback is needed: the scaling keeps every operand inside fp16.
 #include "nrms_common.hpp"
 #include "packs.hpp"
 
@@ -42,18 +52,22 @@ constexpr int USTAMP_FLOATS = 4096 * 8 * 2;     // probe: 8 u64 per user (B <= 4
 constexpr int USTAMP_FLOATS = 0;
 #endif
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 uf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 uf16x4 __attribute__((ext_vector_type(4)));
 
 
 // W_add -> B fragments. x6: element i of lane (n = lane & 15, kq = lane >> 4)
 // is k = 32 ks + 4 kq + (i & 3) + 16 (i >> 2), three bf16 planes. f32: the
 // 16x16x4 layout of the news kernel, k = 16 kg + 4 kq + t.
 __global__ __launch_bounds__(256) void pack_user_b_kernel(const float* __restrict__ Wa,
-                                                          float* __restrict__ WaP, int x6) {
-  pk::pack_user_additive(blockIdx.x * 256 + threadIdx.x, Wa, WaP, x6);
+                                                          float* __restrict__ WaP, int mode) {
+  if (mode == 2) pk::pack_user_additive_h3(blockIdx.x, threadIdx.x, Wa, WaP);
+  else pk::pack_user_additive(blockIdx.x * 256 + threadIdx.x, Wa, WaP, mode);
 }
 static_assert(pk::KS == UKS && pk::NT == UNT && pk::KG == UKG && pk::Q == UQ && pk::D == UD &&
                   pk::USER_F32_ELEMS == UWAP1,
               "packs.hpp layout");
+static_assert(pk::USER_H3_EXP + pk::NT * 16 <= UWAP_MAX, "split-f16 W_add pack fits the workspace");
 
 __device__ __forceinline__ float urow16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
@@ -97,6 +111,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   float* tile = ulds;                                  // [LMAX][URS]
   float* part = tile + LMAX * URS;                     // [UNT][64]
   float* wts = part + UNT * 64;                        // [64]
+  int32_t* rmax = reinterpret_cast<int32_t*>(wts + 64);  // MODE 2: [64] row max |ctx| (float bits)
+  int32_t* rexp = rmax + 64;                           // MODE 2: [64] row exponent ea
   const int64_t s = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -137,6 +153,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       if (e < L * KV4) *reinterpret_cast<float4*>(tile + i * URS + 4 * c) = buf[k];
     }
   }
+  if constexpr (MODE == 2)
+    if (tid < 64) rmax[tid] = 0;
   __syncthreads();
   NRMS_U_STAMP(0)   // K|V staged
 
@@ -206,10 +224,44 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         acc[4 * t + 3] = fmaf(a, v4.w, acc[4 * t + 3]);
       }
     }
+    if constexpr (MODE == 2) {
+      float m = 0.f;
+#pragma unroll
+      for (int t = 0; t < UDK; ++t) m = fmaxf(m, fabsf(acc[t]));
+      atomicMax(rmax + qi, __float_as_int(m));   // (m >= 0: int order = float order)
+    }
   }
   __syncthreads();   // every K|V read done: the tile becomes the context
   NRMS_U_STAMP(1)   // attention
-  if constexpr (MODE == 1) {
+  if constexpr (MODE == 2) {
+    // three fp16 planes per row (hi | lo | r), in the MODE 1 positions
+    _Float16* t16 = reinterpret_cast<_Float16*>(tile);
+    if (has) {
+      const int ea = pk::exp_field(__int_as_float(rmax[qi])) - 3;
+      if (h == 0) rexp[qi] = ea;
+#pragma unroll
+      for (int g = 0; g < UDK / 4; ++g) {
+        _Float16 hv[3][4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          const float v = ldexpf(acc[4 * g + x], -ea);
+          hv[0][x] = (_Float16)v;
+          const float r1 = (v - (float)hv[0][x]) * kF16LoScale;   // exact
+          hv[1][x] = (_Float16)r1;
+          hv[2][x] = (_Float16)(r1 - (float)hv[1][x]);
+        }
+        const int pos = qi * (2 * URS) + ukpos(UDK * h + 4 * g);
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+          *reinterpret_cast<uf16x4*>(t16 + pos + UKP * pl) = uf16x4{hv[pl][0], hv[pl][1], hv[pl][2], hv[pl][3]};
+      }
+    }
+    uint16_t* z16 = reinterpret_cast<uint16_t*>(tile);
+    for (int e = tid; e < L * 15; e += NT) {   // K padding 300..319, each plane
+      const int i = e / 15, g = (e % 15) % 5, pl = (e % 15) / 5;
+      *reinterpret_cast<uint2*>(z16 + i * (2 * URS) + UKP * pl + ukpos(UD + 4 * g)) = make_uint2(0u, 0u);
+    }
+  } else if constexpr (MODE == 1) {
     // three bf16 planes per row (plane p at bf16 offset 320 p), k permuted to
     // the MFMA fragment order: lane (lm, kq) of k-step ks reads 16 contiguous
     // bytes per plane (see ukpos)
@@ -248,6 +300,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   if (w < UNT) {
     const int lm = lane & 15, kq = lane >> 4;
     float qv[NTPW], bv[NTPW];
+    [[maybe_unused]] int ewv[NTPW];   // MODE 2: column exponents
 #pragma unroll
     for (int j = 0; j < NTPW; ++j) {
       const int nt = w + NW * j;
@@ -255,6 +308,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       const bool ok = nt < UNT && col < UQ;
       qv[j] = ok ? q_add[col] : 0.f;
       bv[j] = ok ? b_add[col] : 0.f;
+      if constexpr (MODE == 2) ewv[j] = nt < UNT ? reinterpret_cast<const int32_t*>(WaP)[pk::USER_H3_EXP + col] : 0;
     }
     int arow[MT];
 #pragma unroll
@@ -268,7 +322,36 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 #pragma unroll
       for (int j = 0; j < NTPW; ++j) c[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
 
-    if constexpr (MODE == 1) {
+    if constexpr (MODE == 2) {
+      const uf16x8* Bq = reinterpret_cast<const uf16x8*>(WaP) + lane;
+      const _Float16* t16 = reinterpret_cast<const _Float16*>(tile);
+      for (int ks = 0; ks < UKS; ++ks) {
+        uf16x8 a[MT][2];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl)
+            a[mt][pl] = *reinterpret_cast<const uf16x8*>(t16 + 2 * arow[mt] + UKP * pl + 32 * ks + 8 * kq);
+#pragma unroll
+        for (int j = 0; j < NTPW; ++j) {
+          const int nt = w + NW * j;
+          if (nt >= UNT) break;
+          uf16x8 b[2];
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl) b[pl] = Bq[((ks * UNT + nt) * 2 + pl) * 64];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0], b[1], c[mt][j], 0, 0, 0);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][1], b[0], c[mt][j], 0, 0, 0);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0] * (_Float16)kF16LoScale, b[0], c[mt][j], 0,
+                                                                0, 0);
+        }
+      }
+    } else if constexpr (MODE == 1) {
       const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
       const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile);
       for (int ks = 0; ks < UKS; ++ks) {
@@ -323,7 +406,12 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       for (int mt = 0; mt < MT; ++mt) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = urow16_sum(qv[j] * tanhf(c[mt][j][r] + bv[j]));
+          float y = c[mt][j][r];
+          if constexpr (MODE == 2) {
+            const int row = 16 * mt + 4 * kq + r;
+            y = ldexpf(y, rexp[row < L ? row : L - 1] + ewv[j] - 11);
+          }
+          const float p = urow16_sum(qv[j] * tanhf(y + bv[j]));
           if (lm == 0) part[nt * 64 + 16 * mt + 4 * kq + r] = p;
         }
       }
@@ -354,7 +442,17 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       for (int i = par; i < L; i += 2) {
         const float wi = wts[i];
         float4 cv;
-        if constexpr (MODE == 1) {   // hi + mid + lo == the fp32 context exactly
+        if constexpr (MODE == 2) {   // ldexp(hi + 2^-11 (lo + r), ea): the fp32 context (see MODE 2)
+          const _Float16* t16 = reinterpret_cast<const _Float16*>(tile) + i * (2 * URS) + ukpos(4 * u);
+          const uf16x4 p0 = *reinterpret_cast<const uf16x4*>(t16);
+          const uf16x4 p1 = *reinterpret_cast<const uf16x4*>(t16 + UKP);
+          const uf16x4 p2 = *reinterpret_cast<const uf16x4*>(t16 + 2 * UKP);
+          const int ea = rexp[i];
+          cv.x = ldexpf((float)p0[0] + ((float)p1[0] + (float)p2[0]) * kF16LoUnscale, ea);
+          cv.y = ldexpf((float)p0[1] + ((float)p1[1] + (float)p2[1]) * kF16LoUnscale, ea);
+          cv.z = ldexpf((float)p0[2] + ((float)p1[2] + (float)p2[2]) * kF16LoUnscale, ea);
+          cv.w = ldexpf((float)p0[3] + ((float)p1[3] + (float)p2[3]) * kF16LoUnscale, ea);
+        } else if constexpr (MODE == 1) {   // hi + mid + lo == the fp32 context exactly
           const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile) + i * (2 * URS) + ukpos(4 * u);
           const uint2 p0 = *reinterpret_cast<const uint2*>(t16);
           const uint2 p1 = *reinterpret_cast<const uint2*>(t16 + UKP);
@@ -392,7 +490,7 @@ template <int MODE, int LMAX, int NT>
 int32_t launch_user_inst(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
                          PaddingGroups pg) {
-  const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64) * 4;
+  const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64 + 2 * 64) * 4;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>), (int)lds);
   hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
                      ldq, L, wap, b_add, q_add, out, pg);
@@ -425,13 +523,15 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16 || ldq < 3 * UD || ldq % 4)
     return NRMS_ERR_UNSUPPORTED;
-  const int x6 = gemm_arith() != NRMS_GEMM_F32 ? 1 : 0;
-  const int npk = x6 ? UKS * UNT * 64 * 8 : UWAP1;
+  const int ar = gemm_arith();
+  const int mode = ar == NRMS_GEMM_F32 ? 0 : (ar == NRMS_GEMM_SPLIT_F16X3 ? 2 : 1);
   if (!prepacked) {
-    hipLaunchKernelGGL(pack_user_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, wap, x6);
+    const int blocks = mode == 2 ? pk::USER_H3_BLOCKS : ((mode ? UKS * UNT * 64 * 8 : UWAP1) + 255) / 256;
+    hipLaunchKernelGGL(pack_user_b_kernel, dim3(blocks), dim3(256), 0, s, w_add, wap, mode);
     if (int32_t st = launch_status()) return st;
   }
-  if (x6) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
+  if (mode == 2) return launch_user_mode<2>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
+  if (mode == 1) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
   return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
 }
 
