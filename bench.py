@@ -484,7 +484,7 @@ def main():
                   "f16x3": "fp32 (additive GEMM: 2-plane fp16 split, 22-bit operands, 3 products, fp32 "
                            "accumulate, out-of-fp16-range groups recomputed x6; Q|K|V projections: "
                            "power-of-two-scaled fp16 split, A exact in 3 pieces, W 22-bit, 4 products, fp32 "
-                           "accumulate; UserEncoder additive GEMM: 3-way bf16 split, 6 products)"}[args.gemm],
+                           "accumulate; UserEncoder additive GEMM: power-of-two-scaled 2-plane fp16 split, 3 products)"}[args.gemm],
         "data": "synthetic (MIND-shaped stream: counter-hash ids, random-init weights, N(0,1) embedding table)",
         "config": {"workload": workload, "global_batch": B * world,
                    "impressions_per_gpu": B, "candidates": C, "clicked": N_CLICKED,

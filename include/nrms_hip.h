@@ -101,8 +101,9 @@ typedef enum { NRMS_PROJ_AUTO = 0, NRMS_PROJ_DIRECT = 1, NRMS_PROJ_FOLDED = 2 } 
  * range (exact, any magnitude), split the input exactly into three fp16
  * pieces and the weights into two (22 bits), and accumulate four products:
  * fp32-GEMM accuracy, and products as exact as fp32's for weights that fit
- * in 11 bits. The staged nrms_qkv_project and the UserEncoder's additive GEMM
- * run SPLIT_BF16X6 in this mode.
+ * in 11 bits. The fused UserEncoder's additive GEMM scales each context row
+ * the same way and accumulates three fp16 products (22-bit operands). The
+ * staged nrms_qkv_project and the stage kernels run SPLIT_BF16X6 in this mode.
  * F32: v_mfma_f32_16x16x4_f32, each product an exact fp32 FMA.
  * Process-wide; the initial value comes from the environment (NRMS_GEMM=f32
  * selects F32, NRMS_GEMM=x6 SPLIT_BF16X6). Returns the previous mode, or
