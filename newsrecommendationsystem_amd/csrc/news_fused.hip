@@ -91,15 +91,16 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // Split-f16 x3 variant (F16X3, main pass only): the context and Wa are split
 // into two fp16 planes, a = hi + 2^-11 lo (hi = fp16(a), lo = fp16((a - hi)
 // 2^11): 11 + 11 significand bits; the scaled residual stays normal down to
-// |a| ~ 6e-5 and never overflows where hi does not). Wa also keeps a third
-// plane, hi' = 2^11 hi (exact), so the three products lo·hi, hi·lo, hi·hi'
-// all carry the factor 2^11 and sum in ONE fp32 accumulator on
+// |a| ~ 6e-5 and never overflows where hi does not). Wa's third operand,
+// hi' = 2^11 hi (exact), is formed in registers from the hi plane (the pack
+// also stores it; the kernel loads two planes), so the three products lo·hi,
+// hi·lo, hi·hi' all carry the factor 2^11 and sum in ONE fp32 accumulator on
 // v_mfma_f32_16x16x32_f16 (exact fp16 products): Y = 2^-11 acc. The dropped
 // lo·lo term and the operand residuals are ~2^-22 |a||b| — normwise error
 // below a plain fp32 GEMM's at half the x6 MFMA count.
 // fp16's range is the price. A context value at or beyond 65,520 becomes inf
 // in hi and -inf in lo, so lo·hi + hi·hi' is inf - inf = NaN in every output
-// column of its row; a weight with |hi'| past fp16 is packed as NaN. Either
+// column of its row; a weight with |hi'| past fp16 has NaN packed in hi. Either
 // way the row's score is NaN, and the score check in C routes the group to
 // the recheck pass (x6 + reference exp), as it does for NaN inputs.
 // Row stride 720 halves = 360 dwords (= 40 mod 64, 8 mod 32): the same bank
@@ -725,18 +726,23 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         int bvoff[4];   // lane + N-tile in the VGPR offset; k-step in soffset; plane immediate
 #pragma unroll
         for (int j = 0; j < 4; ++j) bvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
-        // B plane pb: 0 = hi', 1 = lo, 2 = hi; loaded in consumption order
+        // B plane pb: 0 = hi' (formed in registers from hi: 2,048 hi is exact,
+        // and the pack stores NaN in hi where it would pass fp16's range; the
+        // packed hi' plane is not read — 2/3 of the fragment loads: news_fused
+        // -2 %), 1 = lo, 2 = hi; loaded in consumption order
         auto load_b = [&](int ks, f16x8 (&dst)[4][3]) {
 #pragma unroll
-          for (int pl = 2; pl >= 0; --pl)
+          for (int pl = 2; pl >= 1; --pl)
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               dst[j][pl] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(
                   brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
         };
-        auto kstep = [&](int ks, const f16x8 (&bb)[4][3], auto wc) {
+        auto kstep = [&](int ks, f16x8 (&bb)[4][3], auto wc) {
           constexpr int W = decltype(wc)::value;
           constexpr bool EXTRA = W == 0;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) bb[j][0] = bb[j][2] * (_Float16)kF16LoScale;
           f16x8 a[FMT][2];
 #pragma unroll
           for (int pl = 1; pl >= 0; --pl)

@@ -64,7 +64,7 @@ __device__ __forceinline__ void pack_news_additive(int idx, const float* __restr
     const float hs = (float)h * kLoScale;   // exact unless it overflows fp16: NaN then (-> recheck)
     o2[0] = fabsf(hs) < 65504.f ? (_Float16)hs : (_Float16)qnan();
     o2[64 * 8] = (_Float16)((v - (float)h) * kLoScale);
-    o2[2 * 64 * 8] = h;
+    o2[2 * 64 * 8] = fabsf(hs) < 65504.f ? h : (_Float16)qnan();   // (NaN too: hi' may be formed from it)
   }
 }
 
