@@ -200,14 +200,17 @@ struct GroupList {
 
 // One thread per title (10 x 16-B id loads), the 4 lanes of a group combined
 // by a ballot: classify each group (all 80 ids zero; slots past n_titles count
-// as padding) and append the others to the list; one atomic per block.
-__global__ __launch_bounds__(256) void classify_groups_kernel(RowMap rm, int64_t n_groups,
-                                                              int32_t* __restrict__ list,
-                                                              int32_t* __restrict__ count,
-                                                              int32_t* __restrict__ rep,
-                                                              uint8_t* __restrict__ pad_group) {
-  __shared__ int wcount[4], wbase[4], wrep[4];
-  const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;   // title
+// as padding) and append the others to the list; one atomicAdd and one
+// atomicMin per 1,024-title block (device-scope atomics on one address
+// serialise: 256-title blocks took 8.8 us at config 3).
+constexpr int CLS_T = 1024, CLS_W = CLS_T / 64;
+__global__ __launch_bounds__(CLS_T) void classify_groups_kernel(RowMap rm, int64_t n_groups,
+                                                                int32_t* __restrict__ list,
+                                                                int32_t* __restrict__ count,
+                                                                int32_t* __restrict__ rep,
+                                                                uint8_t* __restrict__ pad_group) {
+  __shared__ int wcount[CLS_W], wbase[CLS_W], wrep[CLS_W];
+  const int64_t s = (int64_t)blockIdx.x * CLS_T + threadIdx.x;   // title
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   int64_t any = 0;
   if (s < rm.n_titles) {
@@ -231,11 +234,14 @@ __global__ __launch_bounds__(256) void classify_groups_kernel(RowMap rm, int64_t
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    const int r = min(min(wrep[0], wrep[1]), min(wrep[2], wrep[3]));
+    int r = INT32_MAX, tot = 0;
+    for (int i = 0; i < CLS_W; ++i) {
+      r = min(r, wrep[i]);
+      tot += wcount[i];
+    }
     if (r != INT32_MAX) atomicMin(rep, r);
-    const int tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
     int b = tot ? atomicAdd(count, tot) : 0;
-    for (int i = 0; i < 4; ++i) { wbase[i] = b; b += wcount[i]; }
+    for (int i = 0; i < CLS_W; ++i) { wbase[i] = b; b += wcount[i]; }
   }
   __syncthreads();
   if (lead && !pad) list[wbase[w] + __popcll(keep & ((1ull << lane) - 1))] = (int32_t)g;
@@ -260,34 +266,44 @@ __global__ __launch_bounds__(256) void broadcast_padding_kernel(const uint8_t* _
 // than rep, whose news vectors are copies of rep's slot m % 4 (the UserEncoder
 // reads those rows from 4 rep + m % 4 instead). Appended in any order (vector
 // atomics, one per wave); the count must start at 0.
-// One 256-thread block lists rows m0 .. m0 + 255.
+// One 256-thread block lists rows m0 .. m0 + URL_ROWS - 1 (four 256-row
+// chunks), with one atomic (per-wave atomics on the one counter serialised:
+// 11 us; one per 256 rows: ~200 at config 3).
+constexpr int URL_ROWS = 1024, URL_C = URL_ROWS / 256;
 __device__ __forceinline__ void user_row_list_block(const uint8_t* __restrict__ pad_group,
                                                     const int32_t* __restrict__ rep, int64_t n_rows,
                                                     int64_t* __restrict__ list, int32_t* __restrict__ count,
                                                     int64_t m0) {
-  // one atomic per block (per-wave atomics on the one counter serialised: 11 us)
-  __shared__ int wcount[4], wbase[4];
-  const int64_t m = m0 + threadIdx.x;
+  __shared__ int wcount[URL_C * 4], wbase[URL_C * 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t g = m >> 2;
-  const bool keep = m < n_rows && !(pad_group[g] && g != (int64_t)*rep);
-  const uint64_t ballot = __ballot(keep);
-  if (lane == 0) wcount[w] = __popcll(ballot);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
-    int b = tot ? atomicAdd(count, tot) : 0;
-    for (int i = 0; i < 4; ++i) { wbase[i] = b; b += wcount[i]; }
+  const int64_t r = (int64_t)*rep;
+  bool keep[URL_C];
+  uint64_t ballot[URL_C];
+#pragma unroll
+  for (int c = 0; c < URL_C; ++c) {
+    const int64_t m = m0 + 256 * c + threadIdx.x, g = m >> 2;
+    keep[c] = m < n_rows && !(pad_group[g] && g != r);
+    ballot[c] = __ballot(keep[c]);
+    if (lane == 0) wcount[4 * c + w] = __popcll(ballot[c]);
   }
   __syncthreads();
-  if (keep) list[wbase[w] + __popcll(ballot & ((1ull << lane) - 1))] = m;
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int i = 0; i < URL_C * 4; ++i) tot += wcount[i];
+    int b = tot ? atomicAdd(count, tot) : 0;
+    for (int i = 0; i < URL_C * 4; ++i) { wbase[i] = b; b += wcount[i]; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int c = 0; c < URL_C; ++c)
+    if (keep[c]) list[wbase[4 * c + w] + __popcll(ballot[c] & ((1ull << lane) - 1))] = m0 + 256 * c + threadIdx.x;
 }
 
 __global__ __launch_bounds__(256) void user_row_list_kernel(const uint8_t* __restrict__ pad_group,
                                                             const int32_t* __restrict__ rep,
                                                             int64_t n_rows, int64_t* __restrict__ list,
                                                             int32_t* __restrict__ count) {
-  user_row_list_block(pad_group, rep, n_rows, list, count, (int64_t)blockIdx.x * 256);
+  user_row_list_block(pad_group, rep, n_rows, list, count, (int64_t)blockIdx.x * URL_ROWS);
 }
 
 // The UserEncoder's row list, built by the deduplicating main pass itself
@@ -393,7 +409,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   static_assert(!(H3 && EXACT), "the F16X3 main pass is rechecked by the x6 kernel");
   if constexpr (!EXACT) {
     if (ur.list)   // (workgroup-uniform; the padding classification ran in an earlier launch)
-      for (int64_t m0 = (int64_t)blockIdx.x * NTHR; m0 < ur.n_rows; m0 += (int64_t)gridDim.x * NTHR) {
+      for (int64_t m0 = (int64_t)blockIdx.x * URL_ROWS; m0 < ur.n_rows; m0 += (int64_t)gridDim.x * URL_ROWS) {
         user_row_list_block(ur.pad_group, ur.rep, ur.n_rows, ur.list, ur.count, m0);
         __syncthreads();   // (the block's LDS counters are reused)
       }
@@ -1010,8 +1026,8 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   const int64_t blocks = n_groups < n_cu ? n_groups : n_cu;   // persistent: one workgroup per CU
   RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows};
   if (dedupe) {
-    hipLaunchKernelGGL(classify_groups_kernel, dim3((unsigned)((4 * n_groups + 255) / 256)), dim3(256), 0,
-                       s, rm, n_groups, glist, rcount + 1, rcount + 2, pad_group);
+    hipLaunchKernelGGL(classify_groups_kernel, dim3((unsigned)((4 * n_groups + CLS_T - 1) / CLS_T)), dim3(CLS_T),
+                       0, s, rm, n_groups, glist, rcount + 1, rcount + 2, pad_group);
     if (int32_t st = launch_status()) return st;
   }
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, gl, ws,
@@ -1045,7 +1061,7 @@ PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles) {
 int32_t launch_user_row_list(const PaddingGroups& pg, int64_t n_rows, int64_t* list, hipStream_t s) {
   if (n_rows == 0) return NRMS_OK;
   int32_t* count = pg.user_count;
-  hipLaunchKernelGGL(user_row_list_kernel, dim3((unsigned)((n_rows + 255) / 256)), dim3(256), 0, s,
+  hipLaunchKernelGGL(user_row_list_kernel, dim3((unsigned)((n_rows + URL_ROWS - 1) / URL_ROWS)), dim3(256), 0, s,
                      pg.pad_group, pg.rep, n_rows, list, count);
   return launch_status();
 }
