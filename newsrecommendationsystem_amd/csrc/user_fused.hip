@@ -24,8 +24,10 @@
 //   3. softmax over the N rows (max-subtracted, F.softmax) and the pooling
 //      (two lanes per float4 column, combined by a lane shuffle).
 // MODE 2 (split-f16, the default arithmetic): each context row is scaled by
-// a power of two, 2^-ea (its max |value| into [2^3, 2^4), from an LDS
-// atomic max over the row's 15 head threads), and stored as three fp16
+// a power of two, 2^-ea (its max |value| into [2^3, 2^4): each (head,
+// query) thread leaves its max in an LDS slot, read by the row's 15 threads
+// after the barrier — an LDS atomic kept the row index live across the
+// attention and spilled), and stored as three fp16
 // planes, 2^11 a' = 2^11 hi + lo + r (exact for every value within 2^-15 of
 // the row max; the pooling rebuilds the context from them); W_add comes split
 // per output column (packs.hpp pack_user_additive_h3). The GEMM reads two
@@ -111,8 +113,9 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   float* tile = ulds;                                  // [LMAX][URS]
   float* part = tile + LMAX * URS;                     // [UNT][64]
   float* wts = part + UNT * 64;                        // [64]
-  int32_t* rmax = reinterpret_cast<int32_t*>(wts + 64);  // MODE 2: [64] row max |ctx| (float bits)
-  int32_t* rexp = rmax + 64;                           // MODE 2: [64] row exponent ea
+  // MODE 2: part | wts | [64] hold one max |ctx| per (head, query) thread
+  // until the split; then [64] row exponents ea
+  int32_t* rexp = reinterpret_cast<int32_t*>(wts + 128);
   const int64_t s = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -153,8 +156,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       if (e < L * KV4) *reinterpret_cast<float4*>(tile + i * URS + 4 * c) = buf[k];
     }
   }
-  if constexpr (MODE == 2)
-    if (tid < 64) rmax[tid] = 0;
+  static_assert(MODE != 2 || UNT * 64 + 64 + 64 >= UH * LMAX, "per-thread max slots before rexp");
   __syncthreads();
   NRMS_U_STAMP(0)   // K|V staged
 
@@ -228,7 +230,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       float m = 0.f;
 #pragma unroll
       for (int t = 0; t < UDK; ++t) m = fmaxf(m, fabsf(acc[t]));
-      atomicMax(rmax + qi, __float_as_int(m));   // (m >= 0: int order = float order)
+      part[tid] = m;   // (one slot per (head, query) thread in part | wts | rmax; the row max after the barrier)
     }
   }
   __syncthreads();   // every K|V read done: the tile becomes the context
@@ -237,7 +239,9 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     // three fp16 planes per row (hi | lo | r), in the MODE 1 positions
     _Float16* t16 = reinterpret_cast<_Float16*>(tile);
     if (has) {
-      const int ea = pk::exp_field(__int_as_float(rmax[qi])) - 3;
+      float mx = 0.f;
+      for (int hh = 0; hh < UH; ++hh) mx = fmaxf(mx, part[hh * L + qi]);   // the row's 15 head threads
+      const int ea = pk::exp_field(mx) - 3;
       if (h == 0) rexp[qi] = ea;
 #pragma unroll
       for (int g = 0; g < UDK / 4; ++g) {
