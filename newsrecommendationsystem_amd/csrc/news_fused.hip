@@ -448,14 +448,33 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   // row_of (threads < 80), the pointer stored later by store_row, so the id
   // load's latency hides behind the work in between.
   const int64_t n_groups = (rmap.n_titles + FT - 1) / FT;
-  auto row_of = [&](int64_t tg) -> int64_t {
-    if (tid >= FROWS) return -2;
-    const int t = tid / FL;
-    return rmap(tg * FT + t, tid - t * FL);
+  // row_of issues the id load unconditionally (a safe address where there is
+  // no id) and returns the raw value; store_row, at the end of phase A,
+  // recomputes the title / token from tg and maps it (out of range: NaN row,
+  // past the titles: zero row) — a use or a branch right after the load made
+  // the wait for it land at the start of the phase
+  auto tok = [&](int64_t tg, int64_t& s_, int& i_) __attribute__((always_inline)) -> bool {
+    int tl = tid;
+    asm volatile("" : "+v"(tl));   // (recomputed: a hoisted 64-bit token index spilled)
+    const int t = tl / FL;
+    i_ = tl - t * FL;
+    s_ = tg * FT + t;
+    return tl < FROWS && s_ < rmap.n_titles;
   };
-  auto store_row = [&](int64_t row, int buf) {
+  auto row_of = [&](int64_t tg) -> int64_t {
+    int64_t s_;
+    int i_;
+    const bool ok = tok(tg, s_, i_) && rmap.ids_a;
+    const int64_t* ip = ok ? rmap.ids_of(s_) + i_ : reinterpret_cast<const int64_t*>(WaP);
+    return *ip;
+  };
+  auto store_row = [&](int64_t raw, int64_t tg, int buf) {
+    int64_t s_;
+    int i_;
+    const bool ok = tok(tg, s_, i_);
+    const int64_t r = rmap.ids_a ? raw : s_ * FL + i_;
     if (tid < FROWS)
-      rowptr[buf * FROWS + tid] = row >= 0 ? qkv + row * ldq : (row == -1 ? nan_row : zero_row);
+      rowptr[buf * FROWS + tid] = !ok ? zero_row : ((uint64_t)r < (uint64_t)rmap.n_rows ? qkv + r * ldq : nan_row);
   };
 
   // attention roles: block b = (title t, head slot hl), lane x within the block
@@ -527,7 +546,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     if (gl.list) return k < n_list ? (int64_t)gl.list[k] : (k == n_list && rep != INT32_MAX ? (int64_t)rep : n_groups);
     else return k;
   };
-  if (blockIdx.x < n_iter) store_row(row_of(group_at(blockIdx.x)), 0);
+  if (blockIdx.x < n_iter) store_row(row_of(group_at(blockIdx.x)), group_at(blockIdx.x), 0);
   __syncthreads();
   if (blockIdx.x < n_iter) {
     prefetch_qk(0);
@@ -557,7 +576,8 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       // epilogue (past the last group: zero rows, so the prefetch is
       // unconditional and its registers are dead during the GEMM); stored at
       // the end of this phase
-      const int64_t next_row = row_of(group_at(k + gridDim.x));
+      const int64_t next_tg = group_at(k + gridDim.x);
+      const int64_t next_row = row_of(next_tg);
       // S^T tiles: rows = keys 4j + r (A = K), cols = queries 4i + x (B = Q)
       floatx4 S[5][5];
 #pragma unroll
@@ -655,7 +675,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         o_mfma(i);
         o_store(i);
       }
-      store_row(next_row, nbuf);
+      store_row(next_row, next_tg, nbuf);
     }
     NRMS_STAMP(1)
     __syncthreads();   // context tile complete
