@@ -150,11 +150,19 @@ int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_id
                          const nrms_encoder_weights_t* w, float* qkv, int64_t ld_qkv,
                          hipStream_t stream);
 
-/* Same rows, bitwise, through the workspace: for the NRMS shape (D = 300,
- * split arithmetic) the weight is split into bf16 planes once per call
- * (workspace) and one persistent workgroup per CU keeps a 64-row tile of x
- * resident in LDS while it streams the planes from L2 — the projection the
- * encode / forward entry points use. Other shapes / NRMS_GEMM_F32: as
+/* The same projection through the workspace — the one the encode / forward
+ * entry points use. For the NRMS shape (D = 300, split arithmetic) the weight
+ * is split once per call into MFMA fragments (workspace) and one persistent
+ * workgroup per CU keeps a 64-row tile of x resident in LDS while it streams
+ * the fragments from L2. Bitwise equal to nrms_qkv_project under
+ * NRMS_GEMM_SPLIT_BF16X6 (same x6 products in the same order) and under
+ * NRMS_GEMM_F32 (both run the f32 GEMM). Under NRMS_GEMM_SPLIT_F16X3 (the
+ * default) it runs the scaled split-f16 arithmetic instead — each x row and
+ * each weight row scaled by a power of two into fp16's range, x split exactly
+ * into three fp16 pieces, the weight into two (22 bits), four products summed
+ * in fp32: within ~2^-22 |x||w| per product of the exact result (fp32-GEMM
+ * accuracy; exact products for weights that fit in 11 bits) — so only within
+ * rounding of nrms_qkv_project's x6 rows, not bitwise. Other shapes: as
  * nrms_qkv_project. */
 size_t nrms_qkv_project_workspace_size(int32_t D);
 int32_t nrms_qkv_project_ws(const float* x, int64_t n_rows_x, const int64_t* row_ids, int64_t M,

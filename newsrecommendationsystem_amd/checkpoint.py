@@ -52,12 +52,21 @@ def latest_checkpoint(directory):
 def resume(path, model, optimizer=None):
     """Load model (and optimizer) state as src/train.py:144-159 does; returns
     (step, early_stop_value). The model keeps its device: tensors are mapped
-    onto it, and the optimizer's state follows its parameters' devices."""
-    dev = next(model.parameters()).device
-    ck = load(path, map_location=dev)
+    onto it, and the optimizer's moments follow its parameters' devices.
+
+    The file is read onto the CPU: load_state_dict copies the parameters onto
+    the model's device, and Optimizer.load_state_dict moves exp_avg /
+    exp_avg_sq to each parameter's device but leaves the 'step' counters where
+    they were loaded -- on the CPU, as the reference keeps them (a CUDA step
+    tensor would cost HipAdam a device-to-host sync per parameter per step)."""
+    ck = load(path, map_location="cpu")
     model.load_state_dict(ck["model_state_dict"])
     if optimizer is not None:
         optimizer.load_state_dict(ck["optimizer_state_dict"])
+        for st in optimizer.state.values():
+            step = st.get("step")
+            if torch.is_tensor(step) and step.device.type != "cpu":
+                st["step"] = step.cpu()
     return int(ck["step"]), ck["early_stop_value"]
 
 

@@ -25,11 +25,10 @@ namespace {
 
 template <int LMAX, int DK, int H, int NT>
 __global__ __launch_bounds__(NT) void mhsa_rawexp_kernel(
-    const float* __restrict__ qkv, int64_t n_rows, const int64_t* __restrict__ ids_a,
+    const float* __restrict__ qkv, int64_t ld, int64_t n_rows, const int64_t* __restrict__ ids_a,
     int64_t n_seq_a, const int64_t* __restrict__ ids_b, int L, float* __restrict__ ctx) {
   extern __shared__ __attribute__((aligned(16))) float kv[];  // [L][2D] then row ids
   constexpr int D = H * DK;
-  constexpr int ld = 3 * D;
   const int64_t s = blockIdx.x;
   const int tid = threadIdx.x;
 
@@ -135,9 +134,9 @@ __global__ __launch_bounds__(NT) void mhsa_rawexp_kernel(
 constexpr int kLongThreads = 256;
 
 __global__ __launch_bounds__(kLongThreads) void mhsa_rawexp_long_kernel(
-    const float* __restrict__ qkv, int64_t n_rows, const int64_t* __restrict__ ids_a,
+    const float* __restrict__ qkv, int64_t ld, int64_t n_rows, const int64_t* __restrict__ ids_a,
     int64_t n_seq_a, const int64_t* __restrict__ ids_b, int L, float* __restrict__ ctx) {
-  constexpr int DK = 20, H = 15, D = H * DK, ld = 3 * D;
+  constexpr int DK = 20, H = 15, D = H * DK;
   extern __shared__ __attribute__((aligned(16))) int64_t lrow[];   // [L] row ids
   const int64_t s = blockIdx.x;
   const int tid = threadIdx.x;
@@ -265,7 +264,7 @@ __global__ __launch_bounds__(kPoolThreads) void additive_pool_kernel(
 }
 
 template <int LMAX, int NT>
-int32_t launch_mhsa_inst(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
+int32_t launch_mhsa_inst(const float* qkv, int64_t ld, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
                          const int64_t* ids_b, int64_t n_seq, int L, float* ctx, hipStream_t s) {
   constexpr int DK = 20, H = 15;
   constexpr int D = H * DK;
@@ -274,29 +273,31 @@ int32_t launch_mhsa_inst(const float* qkv, int64_t n_rows, const int64_t* ids_a,
   ensure_dynamic_lds(reinterpret_cast<const void*>(&mhsa_rawexp_kernel<LMAX, DK, H, NT>),
                      160 * 1024);
   hipLaunchKernelGGL((mhsa_rawexp_kernel<LMAX, DK, H, NT>), dim3((unsigned)n_seq), dim3(NT), lds,
-                     s, qkv, n_rows, ids_a, n_seq_a, ids_b, L, ctx);
+                     s, qkv, ld, n_rows, ids_a, n_seq_a, ids_b, L, ctx);
   return launch_status();
 }
 
 }  // namespace
 
-int32_t launch_mhsa(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
+int32_t launch_mhsa(const float* qkv, int64_t ld, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
                     const int64_t* ids_b, int64_t n_seq, int L, int H, int DK, float* ctx,
                     hipStream_t s) {
   if (n_seq == 0) return NRMS_OK;
   // Compiled for the reference configuration: d_k = 20, 15 heads (config.py:34,45).
   if (DK != 20 || H != 15 || L < 1 || L > kMaxSeqLen) return NRMS_ERR_UNSUPPORTED;
+  // q|k|v rows: [q D | k D | v D] at any row stride that keeps the float4 slices aligned
+  if (ld < 3 * (int64_t)H * DK || ld % 4 != 0) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv % 16) != 0 || ((uintptr_t)ctx % 16) != 0) return NRMS_ERR_UNSUPPORTED;
   if (n_seq > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   if (L > 64) {
     hipLaunchKernelGGL(mhsa_rawexp_long_kernel, dim3((unsigned)n_seq), dim3(kLongThreads),
-                       (size_t)L * sizeof(int64_t), s, qkv, n_rows, ids_a, n_seq_a, ids_b, L, ctx);
+                       (size_t)L * sizeof(int64_t), s, qkv, ld, n_rows, ids_a, n_seq_a, ids_b, L, ctx);
     return launch_status();
   }
-  if (L <= 20) return launch_mhsa_inst<20, 320>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
-  if (L <= 32) return launch_mhsa_inst<32, 512>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
-  if (L <= 50) return launch_mhsa_inst<50, 768>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
-  return launch_mhsa_inst<64, 1024>(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
+  if (L <= 20) return launch_mhsa_inst<20, 320>(qkv, ld, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
+  if (L <= 32) return launch_mhsa_inst<32, 512>(qkv, ld, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
+  if (L <= 50) return launch_mhsa_inst<50, 768>(qkv, ld, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
+  return launch_mhsa_inst<64, 1024>(qkv, ld, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, ctx, s);
 }
 
 int32_t launch_additive_pool(const float* x, const float* score, int64_t n_seq, int L, int D,

@@ -148,8 +148,9 @@ int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int
     return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
                              w->q_add, wap, out, s, -1, deduped, broadcast_from, user_list, user_rows,
                              prepacked);
-  if (ldq != 3 * (int64_t)D) return NRMS_ERR_UNSUPPORTED;   // stage kernels: packed rows
-  int32_t st = launch_mhsa(qkv, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
+  // stage kernels: any row stride >= 3D (packed rows, or the folded table's
+  // padded 128-B-line rows that nrms_qkv_row_stride reports)
+  int32_t st = launch_mhsa(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
   st = launch_gemm_additive_score(ctx, n_seq * L, D, w->w_add, w->b_add, w->q_add, w->query_dim,
                                   scores, s);
@@ -236,7 +237,7 @@ int32_t nrms_self_attention(const float* qkv, int64_t n_rows_qkv, const int64_t*
   if (n_seq < 0 || n_seq_a < 0 || L <= 0) return NRMS_ERR_INVALID_ARG;
   if (int32_t st = shape_ok(w)) return st;
   if (n_seq > 0 && (!qkv || !ctx)) return NRMS_ERR_INVALID_ARG;
-  return launch_mhsa(qkv, n_rows_qkv, tok_ids, n_seq_a, tok_ids_b, n_seq, L, w->n_heads, kDK, ctx,
+  return launch_mhsa(qkv, 3 * (int64_t)w->d_model, n_rows_qkv, tok_ids, n_seq_a, tok_ids_b, n_seq, L, w->n_heads, kDK, ctx,
                      stream);
 }
 

@@ -93,11 +93,13 @@ __device__ __forceinline__ void split3x2(float x0, float x1, uint32_t& hi, uint3
 // 65,520 gives hi = inf, lo = -inf, and every product sum it enters becomes
 // NaN. The weight side also keeps hi' = 2^11 hi (NaN where that overflows,
 // |w| >= 32), so lo·hi + hi·lo + hi·hi' = 2^11 x·w in one accumulator.
-// Used for the additive projections only: their outputs feed tanh and a
-// max-subtracted softmax, so ulp-level operand rounding has no boundary
-// effects there; the Q|K|V projections stay x6, whose exact operand split
-// keeps single-term products (and so the raw-exp overflow boundary of the
-// attention scores) bit-exact with the reference.
+// Used for the additive projections (news and UserEncoder): their outputs
+// feed tanh and a max-subtracted softmax, so ulp-level operand rounding has no
+// boundary effects there. The Q|K|V projections do not use this two-plane
+// form: under SPLIT_F16X3 they scale rows into fp16's range and split the
+// input exactly into three pieces (proj_x6.hip), so single-term products --
+// and with them the raw-exp overflow boundary of the attention scores -- stay
+// bit-exact with the reference.
 constexpr float kF16LoScale = 2048.0f, kF16LoUnscale = 1.0f / 2048.0f;
 typedef _Float16 nrms_f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 nrms_f16x4 __attribute__((ext_vector_type(4)));
@@ -194,7 +196,9 @@ int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& w
 int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
                                    const float* b, const float* q, int N, float* score,
                                    hipStream_t s);
-int32_t launch_mhsa(const float* qkv, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
+// ld: q|k|v row stride in floats (>= 3 H DK, a multiple of 4: the padded
+// folded table of nrms_qkv_row_stride works as well as packed 3D rows)
+int32_t launch_mhsa(const float* qkv, int64_t ld, int64_t n_rows, const int64_t* ids_a, int64_t n_seq_a,
                     const int64_t* ids_b, int64_t n_seq, int L, int H, int DK, float* ctx,
                     hipStream_t s);
 int32_t launch_additive_pool(const float* x, const float* score, int64_t n_seq, int L, int D,

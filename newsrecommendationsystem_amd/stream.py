@@ -46,8 +46,16 @@ def _uniform_int(h, lo, hi):
     return lo + _srl(h, 11) % (hi - lo)
 
 
+def _wrap64(v):
+    """A Python int reduced to a signed int64 (two's-complement wrap), as the
+    tensor arithmetic would wrap it."""
+    return ((int(v) + (1 << 63)) % (1 << 64)) - (1 << 63)
+
+
 def _key(seed, stream, x):
-    return mix(mix(x + (seed * 1_000_003 + stream) * 0x1000000000))
+    # the seed term wraps to int64 first: any seed is valid (unchanged values
+    # for the small seeds, where nothing wrapped)
+    return mix(mix(x + _wrap64((seed * 1_000_003 + stream) * 0x1000000000)))
 
 
 def impression_users(seed, k, n_users=N_USERS):

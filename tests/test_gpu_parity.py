@@ -242,6 +242,24 @@ def test_news_encoder_title_lengths_vs_oracle(device, L):
     assert O.normwise_rel_err(out, ref).max() < TOL
 
 
+@pytest.mark.parametrize("L", [5, 20, 32, 50])
+def test_news_encoder_cached_folded_table_title_lengths(device, L):
+    """The eval path with the default cached folded table (padded 128-B-line
+    rows, nrms_qkv_row_stride) at title lengths the fused kernel does not take:
+    the stage kernels read the padded rows (L != 20 used to fail)."""
+    V = 512
+    sd = W.nrms_state(7, V)
+    m = _module(sd, V, device)
+    assert getattr(m.config, "hip_cache_folded_table", True)
+    ids = W.titles(7, 700 + L, 29, V, L=L, min_len=1)
+    with torch.no_grad():
+        out = _np(m.get_news_vector({"title": torch.from_numpy(ids)}))
+        again = _np(m.get_news_vector({"title": torch.from_numpy(ids)}))   # cached table reused
+    ref = O.news_encode(ids, sd, np.float64)
+    assert O.normwise_rel_err(out, ref).max() < TOL
+    assert np.array_equal(out, again)
+
+
 def test_empty_batch(gold_model):
     with torch.no_grad():
         out = gold_model.get_news_vector({"title": torch.zeros(0, 20, dtype=torch.long)})
@@ -760,6 +778,42 @@ def test_padding_title_dedupe_is_bitwise_identical(device, pad_frac, gemm_mode):
     if pad.any():   # one vector per slot; slots agree to fp32 rounding
         vp = outs[1][1][pad.to(device)]
         assert float((vp - vp[:1]).abs().max()) <= 1e-6 * float(vp.abs().max())
+
+
+def test_padding_title_dedupe_odd_batch_bitwise(device, gemm_mode):
+    """with B = 37 and N = 50 the B*N clicked titles are not a
+    multiple of 4, so the 4-title group holding the last user's final history
+    slots also holds the first user's first candidates. Both are all padding
+    here, plus several whole padding groups elsewhere: the representative
+    group choice, the UserEncoder row list and the scorer's redirect to the
+    representative group all see a group that straddles clicked and candidate
+    titles. Logits must be bitwise equal with the dedupe on and off."""
+    from newsrecommendationsystem_amd import _native as N
+    V, B, N_ = 2500, 37, 50
+    sd = W.nrms_state(67, V)
+    m = _module(sd, V, device, hip_proj_mode=N.NRMS_PROJ_FOLDED)
+    cand, clk, _ = W.impressions(67, 5, B, V, N=N_)
+    cand, clk = cand.copy(), clk.copy()
+    assert (B * N_) % 4 != 0
+    clk[-1, -3:] = 0                 # last user's final history slots
+    cand[0, :2] = 0                  # first user's first candidates (same group)
+    clk[3, :40] = 0                  # whole all-padding groups elsewhere
+    clk[11, :] = 0
+    cand[20, :] = 0
+    lib = N.load()
+    outs = {}
+    prev = lib.nrms_set_title_dedupe(1)
+    try:
+        for on in (1, 0):
+            lib.nrms_set_title_dedupe(on)
+            with torch.no_grad():
+                outs[on] = m.forward_ids(torch.from_numpy(cand), torch.from_numpy(clk)).clone()
+    finally:
+        lib.nrms_set_title_dedupe(prev)
+    assert torch.equal(outs[1], outs[0])
+    assert torch.isfinite(outs[1]).all()
+    ref = O.forward(cand, clk, sd, np.float64)
+    assert np.abs(_np(outs[1]) - ref).max() <= TOL * max(np.abs(ref).max(), 1e-6)
 
 
 def test_forward_graph_replay_recomputes_bitwise(device):
