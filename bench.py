@@ -413,22 +413,29 @@ def main():
         for i, st in enumerate(stages):
             stage_ms[st] += ev[i].elapsed_time(ev[i + 1])
     stage_ms = {st: v / n_ev for st, v in stage_ms.items()}
-    # titles the news tail encodes per step: with padding-title dedupe (library
-    # default, nrms_set_title_dedupe) all-zero titles count once
-    # (nrms_forward orders titles [clicked | candidates]; whole 4-title groups of
-    # padding are skipped, one of them encoded)
+    # titles the news tail encodes per step (nrms_forward orders titles
+    # [clicked | candidates]): with padding-title dedupe (library default,
+    # nrms_set_title_dedupe) the all-zero titles count once (rep = the first);
+    # with token compaction (nrms_set_token_compaction) a title is encoded on
+    # Le = c + (c < 20) distinct q|k|v rows, c = its real (non-zero) tokens
+    lib = Nat.load()
+    compact = bool(lib.nrms_set_token_compaction(1))
+    lib.nrms_set_token_compaction(int(compact))
     all_titles = torch.cat([clk.reshape(-1, L), cand.reshape(-1, L)])
     n_titles = all_titles.shape[0]
-    n_pad = int((all_titles == 0).all(-1).sum())
-    grp = torch.nn.functional.pad((all_titles != 0).any(-1), (0, (-n_titles) % 4)).view(-1, 4).any(-1)
-    n_pad_groups = int((~grp).sum())
-    n_enc = 4 * (grp.numel() - n_pad_groups + (1 if n_pad_groups else 0))
+    cnt = (all_titles != 0).sum(-1)
+    pad = cnt == 0
+    n_pad = int(pad.sum())
+    le = torch.where(cnt < L, cnt + 1, cnt) if compact else torch.full_like(cnt, L)
+    le_enc = torch.cat([le[~pad], le[pad][:1]])   # the rep: one all-padding title
+    n_enc = int(le_enc.numel())
+    news_rows = (int(le_enc.sum()), int((le_enc * le_enc).sum()))
     # clicked rows the UserEncoder projects: the copied padding rows are skipped
     n_clk = clk.shape[0] * N_CLICKED
-    clk_pad_groups = int((~grp[: (n_clk + 3) // 4]).sum())
-    n_user = n_clk - 4 * max(clk_pad_groups - 1, 0) if not args.unfused else n_clk
-    work = plan.work(titles_encoded=n_enc if not args.unfused else n_all_titles(B),
-                     user_rows_projected=n_user)
+    clk_pad = int(pad[:n_clk].sum())
+    n_user = n_clk - max(clk_pad - 1, 0) if not args.unfused else n_clk
+    work = (plan.work(titles_encoded=n_enc, user_rows_projected=n_user, news_rows=news_rows)
+            if not args.unfused else plan.work())
     dom = max(stage_ms, key=stage_ms.get)
     w = work[dom]
     t_dom = stage_ms[dom] / 1e3
@@ -470,10 +477,10 @@ def main():
     workload = ("BASELINE cfg4: full NRMS forward over the whole user-sharded stream "
                 f"({idx.numel() if not dist else 'per-rank shards of'} impressions"
                 f"{'' if dist else ' on this GPU'}), every title's vector produced (all-padding "
-                "history groups encoded once per batch, see titles)"
+                "history titles encoded once per batch, see titles)"
                 if args.stream else
                 "BASELINE cfg3: full NRMS forward scoring (news+user encoder+click predictor), "
-                "every title's vector produced (all-padding history groups encoded once per batch, see "
+                "every title's vector produced (all-padding history titles encoded once per batch, see "
                 "titles); batch = first B impressions of this rank's cfg4 user shard")
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "impressions/s", "n_gpus": world,
@@ -495,11 +502,14 @@ def main():
                               "users": S.N_USERS, "sharding": "user_id % world"},
                    "parallelism": f"user-shard x{world}"},
         "roofline": roofline,
-        "titles": {"per_step": n_titles, "all_padding": n_pad, "all_padding_groups": n_pad_groups,
-                   "encoded": n_enc,
-                   "dedupe": "one all-padding 4-title group encoded per step, its slot vectors "
-                             "copied to the other all-padding groups (bitwise identical logits; "
-                             "no_title_dedupe below times every title encoded)"},
+        "titles": {"per_step": n_titles, "all_padding": n_pad, "encoded": n_enc,
+                   "rows_encoded": news_rows[0], "rows_if_uncompacted": n_enc * L,
+                   "token_compaction": compact,
+                   "dedupe": "one all-padding title encoded per step, its vector read by the other "
+                             "all-padding slots (bitwise identical logits: no_title_dedupe below)",
+                   "compaction": "a title's id-0 tokens share one q|k|v row, encoded once with its "
+                                 "multiplicity (news_fused.hip; fp32-rounding-level difference: "
+                                 "no_token_compaction below)"},
         "stages_ms": {st: round(v, 4) for st, v in stage_ms.items()},
         "stages_note": f"HIP events recorded by the library between its stages, a separate pass of "
                        f"{n_ev} steps after the timed ones (events cost queue time, so the timed steps "
@@ -522,19 +532,27 @@ def main():
             with torch.no_grad():
                 y_d = dfwd.run(cand, clk).clone()
                 dms = _time_launches(lambda: dfwd.run(cand, clk), 10, device)
-            lib = Nat.load()
-            prev = lib.nrms_set_title_dedupe(0)
-            try:
-                with torch.no_grad():
-                    y_n = fwd.run(cand, clk).clone()
-                    nms = _time_launches(lambda: fwd.run(cand, clk), 10, device)
-            finally:
-                lib.nrms_set_title_dedupe(prev)
+            def variant(dedupe, compaction):
+                pd, pc = lib.nrms_set_title_dedupe(dedupe), lib.nrms_set_token_compaction(compaction)
+                try:
+                    with torch.no_grad():
+                        y = fwd.run(cand, clk).clone()
+                        ms = _time_launches(lambda: fwd.run(cand, clk), 10, device)
+                finally:
+                    lib.nrms_set_title_dedupe(pd)
+                    lib.nrms_set_token_compaction(pc)
+                return y, ms
+            y_c, cms = variant(1, 0)
+            y_n, nms = variant(0, 0)
+            out["no_token_compaction"] = {
+                "ms_per_step": round(cms, 4), "impressions_per_s": round(B / (cms / 1e3), 1),
+                "max_rel_diff_vs_default": float(((y_c - y_fwd).norm(dim=1) / y_fwd.norm(dim=1)).max()),
+                "note": "every token of a title on its own q|k|v row (nrms_set_token_compaction(0))"}
             out["no_title_dedupe"] = {
                 "ms_per_step": round(nms, 4), "impressions_per_s": round(B / (nms / 1e3), 1),
-                "logits_bitwise_equal": bool(torch.equal(y_n, y_fwd)),
-                "note": "every title encoded and every clicked row projected separately "
-                        "(nrms_set_title_dedupe(0))"}
+                "logits_bitwise_equal_to_no_token_compaction": bool(torch.equal(y_n, y_c)),
+                "note": "every title and every token encoded, every clicked row projected separately "
+                        "(nrms_set_title_dedupe(0) + nrms_set_token_compaction(0))"}
             out["direct_projection"] = {
                 "ms_per_step": round(dms, 4), "impressions_per_s": round(B / (dms / 1e3), 1),
                 "max_rel_diff_vs_folded": float(((y_d - y_fwd).norm(dim=1) / y_fwd.norm(dim=1)).max()),

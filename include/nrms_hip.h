@@ -48,7 +48,9 @@ extern "C" {
  *    holds the UserEncoder row list (nrms_forward_workspace_size grew). */
 /* 4: nrms_qkv_project_ws; the encode / forward workspaces hold the split
  *    Q|K|V weight (their *_workspace_size functions grew). */
-#define NRMS_ABI_VERSION 4
+/* 5: nrms_set_token_compaction; title-level padding dedupe; the encode /
+ *    forward workspaces hold the title buckets (*_workspace_size grew). */
+#define NRMS_ABI_VERSION 5
 
 typedef enum {
   NRMS_OK = 0,
@@ -122,10 +124,24 @@ int32_t nrms_get_gemm_arith(void);
  * have the same news vector. With dedupe on (default), the fused news tail
  * encodes one of them per call and copies its vector to the others; every
  * output is bitwise the same as encoding each title (a title's vector depends
- * on its own ids only). Applies where ids are passed (folded projection).
- * Process-wide, read at enqueue time; returns the previous setting.
- * NRMS_DEDUPE=0 in the environment starts with it off. */
+ * on its own ids only, never on where in the launch it is encoded). Applies
+ * where ids are passed (16-B aligned id rows). Process-wide, read at enqueue
+ * time; returns the previous setting. NRMS_DEDUPE=0 in the environment starts
+ * with it off. */
 int32_t nrms_set_title_dedupe(int32_t on);
+
+/* Token compaction in the fused news tail (default on): the id-0 tokens of a
+ * title (its right-padding, src/data_preprocess.py:115,132-139) share one
+ * q|k|v row, so a title with c real tokens is encoded on c + 1 distinct rows,
+ * the padding row carrying its multiplicity 20 - c in the raw-exp sums, the
+ * attention context and the additive softmax / pooling (news_fused.hip). The
+ * raw-exp row sums are bitwise the uncompacted ones (the padding row's exp is
+ * added 20 - c times, in the reference's key order); the context and pooling
+ * replace 20 - c equal additions by one product: results agree with the
+ * uncompacted computation to fp32 rounding. Process-wide, read at enqueue
+ * time; returns the previous setting. NRMS_COMPACT=0 in the environment
+ * starts with it off. */
+int32_t nrms_set_token_compaction(int32_t on);
 
 int32_t nrms_abi_version(void);
 const char* nrms_status_string(int32_t status);

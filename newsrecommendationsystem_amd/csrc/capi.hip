@@ -141,13 +141,14 @@ int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
                         hipStream_t s, float* wap = nullptr, bool* deduped = nullptr,
                         int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0,
-                        bool prepacked = false) {
+                        bool prepacked = false, bool direct_rows = false) {
   const int D = w->d_model;
   if (deduped) *deduped = false;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
     return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
                              w->q_add, wap, out, s, -1, deduped, broadcast_from, user_list, user_rows,
-                             prepacked);
+                             prepacked, direct_rows);
+  if (direct_rows) ids_a = ids_b = nullptr;   // per-token rows: the ids only classify (fused kernel)
   // stage kernels: any row stride >= 3D (packed rows, or the folded table's
   // padded 128-B-line rows that nrms_qkv_row_stride reports)
   int32_t st = launch_mhsa(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
@@ -176,6 +177,8 @@ int32_t nrms_set_gemm_arith(int32_t mode) {
 int32_t nrms_get_gemm_arith(void) { return gemm_arith(); }
 
 int32_t nrms_set_title_dedupe(int32_t on) { return set_title_dedupe(on); }
+
+int32_t nrms_set_token_compaction(int32_t on) { return set_token_compaction(on); }
 
 const char* nrms_status_string(int32_t st) {
   switch (st) {
@@ -329,8 +332,8 @@ int32_t nrms_news_encode(const int64_t* ids, int64_t n_titles, int32_t L, const 
   // Per-token projection with the embedding gather fused into the A-operand load.
   st = project_qkv(table, V, contiguous_rows(D), ids, n_titles * L, w, pack, false, qkv, ld, stream);
   if (st) return st;
-  return encode_from_qkv(qkv, ld, n_titles * L, nullptr, n_titles, nullptr, n_titles, L, w, ctx,
-                         scores, out, stream, wap);
+  return encode_from_qkv(qkv, ld, n_titles * L, ids, n_titles, nullptr, n_titles, L, w, ctx,
+                         scores, out, stream, wap, nullptr, 0, nullptr, 0, false, /*direct_rows=*/true);
 }
 
 size_t nrms_news_encode_folded_workspace_size(int64_t n_titles, int32_t L, int32_t D) {
@@ -530,8 +533,11 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
                      qkv + (size_t)n_clk * L * ld, ld, stream, nullptr, arith);
     if (st) return st;
     if ((st = rec(1))) return st;
-    st = encode_from_qkv(qkv, ld, n_all * L, nullptr, n_all, nullptr, n_all, L, news_w, ctx,
-                         scores, news, stream, wap);
+    // (the ids only classify the tokens: the rows are per token; the all-padding
+    // titles' copies are written for every title, so the UserEncoder and the
+    // scorer read plain rows)
+    st = encode_from_qkv(qkv, ld, n_all * L, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx,
+                         scores, news, stream, wap, nullptr, 0, nullptr, 0, false, /*direct_rows=*/true);
   }
   if (st) return st;
   if ((st = rec(2))) return st;

@@ -52,13 +52,17 @@ constexpr int FROWS = FT * FL;       // 80 token rows
 constexpr int FD = 300, FH = 15, FDK = 20, FQ = 200;
 constexpr int FKG = 19;              // k-groups of 16 (K = 300 padded to 304)
 constexpr int FNT = 13;              // N tiles of 16 (208 >= Q)
-constexpr int FMT = FROWS / 16;      // 5 M tiles
 constexpr int SC = 328;              // context row stride in floats (== 8 mod 32)
 constexpr int NTHR = 256;
 constexpr int WAP_FLOATS = FKG * FNT * 64 * 4;             // packed Wa
 constexpr int ROW = 3 * FD;                                // q|k|v row: [q 300 | k 300 | v 300]
 constexpr int SPECIAL_FLOATS = 2 * ROW;                    // zero row + NaN row
-constexpr int LDS_FLOATS = FROWS * SC + 4 * FROWS + 2 * 2 * FROWS;   // ctx, partials, rowptr[2] (u64)
+// after the context tile: row partials [80][PART_STRIDE] (the four waves' N-tile
+// sums + the N-tile-12 sum), row pointers [2][80] (u64), title meta [2][8] and
+// the group schedule [16] (int32)
+constexpr int PART_STRIDE = 8;
+constexpr int TAIL_FLOATS = PART_STRIDE * FROWS + 2 * 2 * FROWS + 16 + 16;
+constexpr int LDS_FLOATS = FROWS * SC + TAIL_FLOATS;   // ctx, partials, rowptr, meta
 constexpr size_t LDS_BYTES = LDS_FLOATS * sizeof(float);
 
 // Split-bf16 GEMM variant (X6): the context is stored as three bf16 planes
@@ -82,7 +86,7 @@ constexpr int XKP = XKS * 32;             // 320
 constexpr int XRB = 3 * XKP + NRMS_XRB_PAD;
 constexpr int WAP3_FLOATS = XKS * FNT * 3 * 64 * 4;   // [ks][nt][plane][lane][8 bf16]
 constexpr int WAP_MAX = WAP3_FLOATS > WAP_FLOATS ? WAP3_FLOATS : WAP_FLOATS;
-constexpr size_t LDS_BYTES_X6 = (size_t)FROWS * XRB * 2 + (4 * FROWS + 2 * 2 * FROWS) * sizeof(float);
+constexpr size_t LDS_BYTES_X6 = (size_t)FROWS * XRB * 2 + TAIL_FLOATS * sizeof(float);
 static_assert(LDS_BYTES_X6 <= 160 * 1024, "LDS (x6)");
 static_assert((FROWS * XRB * 2) % 16 == 0 && (XRB * 2) % 16 == 0, "x6 row stride");
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -108,7 +112,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 // plane stores.
 constexpr int XRH = 2 * XKP + 80;
 constexpr int WAP2_FLOATS = XKS * FNT * 3 * 64 * 4;   // [ks][nt][plane hi' | lo | hi][lane][8 f16]
-constexpr size_t LDS_BYTES_H = (size_t)FROWS * XRH * 2 + (4 * FROWS + 2 * 2 * FROWS) * sizeof(float);
+constexpr size_t LDS_BYTES_H = (size_t)FROWS * XRH * 2 + TAIL_FLOATS * sizeof(float);
 static_assert(LDS_BYTES_H <= 160 * 1024 && (XRH / 2) % 64 == 40, "f16x3 row stride");
 constexpr float kLoUnscale = kF16LoUnscale;
 typedef nrms_f16x8 f16x8;
@@ -131,8 +135,8 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
                                                               float* __restrict__ WaP,
                                                               int32_t* __restrict__ recheck_count) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx < 4)   // [recheck count, group-list count, rep, user row-list count]
-    recheck_count[idx] = idx == 2 ? INT32_MAX : 0;
+  if (idx < pk::NEWS_NCOUNT)   // [recheck count, bucket counts x5, rep, user row-list count]
+    recheck_count[idx] = idx == pk::NEWS_CNT_REP ? INT32_MAX : 0;
   if (idx >= WAP_FLOATS + SPECIAL_FLOATS) return;
   if (idx >= WAP_FLOATS) {
     const int sidx = idx - WAP_FLOATS;
@@ -164,16 +168,44 @@ static_assert(pk::NEWS_WAP_MAX == WAP_MAX && pk::NEWS_SPECIAL == SPECIAL_FLOATS 
 static_assert(pk::NEWS_COUNTERS == WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS, "packs.hpp counters");
 
 
+// ------------------------------------------------------------------ titles and rows
+//
+// Token compaction. Every id-0 token of a title (the right-padding of titles
+// shorter than 20 words, src/data_preprocess.py:115,132-139) has the same
+// q|k|v row, so it gives the same attention scores against every key and the
+// same context row as a query. A title with c real tokens (ids != 0) and
+// n_pad = 20 - c padding tokens is therefore encoded on Le = c + (n_pad > 0)
+// distinct rows: its real tokens in order, then ONE padding row (the "rep")
+// that carries the multiplicity n_pad:
+//   raw-exp sums  sum_k e_k: the real keys, the rep, then n_pad - 1 more
+//                 additions of the rep's e, in that order (the reference's key
+//                 order for right padding; the sum, and with it the overflow /
+//                 NaN behaviour of multihead_self.py:16-20, is bitwise the
+//                 uncompacted one);
+//   context       ctx = sum_k P_k v_k with the rep's P scaled by n_pad;
+//   softmax/pool  the rep's score and context row weighted by n_pad
+//                 (additive.py:37-52).
+// Only the summation of n_pad equal terms changes (one product instead of
+// n_pad additions): results agree with the uncompacted computation to fp32
+// rounding. Titles are bucketed by NB = ceil(Le / 4) (blocks of 4 rows, the
+// 4x4x1 MFMA attention's granule) and encoded in groups of 4 titles of one
+// bucket: 16 NB rows, NB M-tiles, NB^2 of the 25 attention tile pairs.
+// Without compaction every title is one 20-row slot (NB = 5).
+constexpr int NBK = 5;                                   // buckets NB = 1..5
+constexpr int NCNT = pk::NEWS_NCOUNT;                    // int32 counters of a launch
+constexpr int CNT_RECHECK = 0, CNT_BUCKET = 1, CNT_REP = pk::NEWS_CNT_REP, CNT_USER = 7;
+static_assert(CNT_BUCKET + NBK == CNT_REP && CNT_USER < NCNT, "counter layout");
+
 struct RowMap {
   const int64_t* ids_a;
   const int64_t* ids_b;
   int64_t n_seq_a, n_titles, n_rows;
-  // q|k|v row of token i of title s: >= 0 row, -1 invalid id (NaN row), -2 padding title
+  bool direct;   // per-token rows s * FL + i (the per-token projection); ids only classify
+  // q|k|v row of token i of title s: >= 0 row, -1 invalid id (NaN row), -2 no title (zero row)
   __device__ __forceinline__ int64_t operator()(int64_t s, int i) const {
-    if (s >= n_titles) return -2;
-    if (!ids_a) return s * FL + i;
-    const int64_t* ids = (s < n_seq_a || ids_b == nullptr) ? ids_a + s * FL : ids_b + (s - n_seq_a) * FL;
-    const int64_t id = ids[i];
+    if (s < 0 || s >= n_titles) return -2;
+    if (direct || !ids_a) return s * FL + i;
+    const int64_t id = ids_of(s)[i];
     return ((uint64_t)id < (uint64_t)n_rows) ? id : -1;
   }
   __device__ __forceinline__ const int64_t* ids_of(int64_t s) const {
@@ -181,96 +213,123 @@ struct RowMap {
   }
 };
 
-// Groups the main pass encodes. Every all-padding title (20 zero ids: the
-// left-padding of short histories, src/dataset.py:79-83) has the same news
-// vector in a given slot of its 4-title group, and padding runs are contiguous
-// (histories are left-padded), so whole groups are padding. With a list, the
-// main pass encodes only the groups holding a real title, plus one
-// all-padding group (rep, the lowest); broadcast_padding_kernel then copies
-// rep's vector of slot s % 4 to every title s of the other all-padding groups.
-// Groups keep their titles and slots, so every output is bitwise the one the
-// undeduplicated launch computes (a row's additive score sums its N-tile
-// partials in an order set by its slot); the list order (atomics) only
-// decides which workgroup encodes which group. Without a list group k is k.
-struct GroupList {
-  const int32_t* list;
-  const int32_t* count;
-  const int32_t* rep;   // INT32_MAX: no all-padding group
+// Classification output (workspace): compacted row ids per title slot, the
+// real-token count, the all-padding flag, per-bucket title lists and counters.
+struct Titles {
+  int32_t* crow;        // [n_titles][FL]: >= 0 row, -1 NaN row (invalid id), -2 zero row (unused slot)
+  uint8_t* cnt;         // [n_titles] c (FL without compaction)
+  uint8_t* pad_title;   // [n_titles] all 20 ids zero
+  int32_t* list;        // [NBK][stride]
+  int32_t* counters;    // [NCNT]
+  int64_t stride;
 };
 
-// One thread per title (10 x 16-B id loads), the 4 lanes of a group combined
-// by a ballot: classify each group (all 80 ids zero; slots past n_titles count
-// as padding) and append the others to the list; one atomicAdd and one
+// One thread per title (10 x 16-B id loads). Lists every title in the bucket
+// of its compacted length, except (dedupe) the all-padding titles: those are
+// one vector, encoded once for the lowest of them (rep, appended to its
+// bucket by the main pass) and copied. One atomicAdd per bucket and one
 // atomicMin per 1,024-title block (device-scope atomics on one address
-// serialise: 256-title blocks took 8.8 us at config 3).
+// serialise). List order is arbitrary: a title's result does not depend on the
+// group or slot it is encoded in.
 constexpr int CLS_T = 1024, CLS_W = CLS_T / 64;
-__global__ __launch_bounds__(CLS_T) void classify_groups_kernel(RowMap rm, int64_t n_groups,
-                                                                int32_t* __restrict__ list,
-                                                                int32_t* __restrict__ count,
-                                                                int32_t* __restrict__ rep,
-                                                                uint8_t* __restrict__ pad_group) {
-  __shared__ int wcount[CLS_W], wbase[CLS_W], wrep[CLS_W];
-  const int64_t s = (int64_t)blockIdx.x * CLS_T + threadIdx.x;   // title
+__global__ __launch_bounds__(CLS_T) void classify_titles_kernel(RowMap rm, Titles tt, int dedupe, int compact) {
+  __shared__ int wcnt[NBK][CLS_W], wbase[NBK][CLS_W], wrep[CLS_W];
+  const int64_t s = (int64_t)blockIdx.x * CLS_T + threadIdx.x;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int64_t any = 0;
+  int bucket = -1;
+  bool allpad = false;
   if (s < rm.n_titles) {
-    const int64_t* ids = rm.ids_of(s);
+    const int4* ids4 = reinterpret_cast<const int4*>(rm.ids_of(s));   // 16-B aligned id rows (checked)
+    int64_t id[FL];
 #pragma unroll
-    for (int i = 0; i < FL; i += 2) {
-      const int4 v = *reinterpret_cast<const int4*>(ids + i);   // 16-B aligned id rows (checked)
-      any |= (int64_t)(v.x | v.y | v.z | v.w);
+    for (int i = 0; i < FL / 2; ++i) {
+      const int4 v = ids4[i];
+      id[2 * i] = (int64_t)(((uint64_t)(uint32_t)v.y << 32) | (uint32_t)v.x);
+      id[2 * i + 1] = (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
     }
+    auto row = [&](int i) -> int32_t {
+      if (rm.direct) return (int32_t)(s * FL + i);
+      return ((uint64_t)id[i] < (uint64_t)rm.n_rows) ? (int32_t)id[i] : -1;
+    };
+    int32_t* cr = tt.crow + s * FL;
+    int c = 0, first_pad = -1;
+    // the rep's row: id 0's (folded) or the first padding token's (per token)
+    auto pad_row = [&](int i) -> int32_t { return rm.direct ? (int32_t)(s * FL + i) : (rm.n_rows > 0 ? 0 : -1); };
+    if (compact) {
+#pragma unroll
+      for (int i = 0; i < FL; ++i) {
+        if (id[i] != 0) cr[c++] = row(i);
+        else if (first_pad < 0) first_pad = i;
+      }
+#pragma unroll
+      for (int q = 0; q < FL; ++q)
+        if (q >= c) cr[q] = q == c ? pad_row(first_pad) : -2;
+      const int le = c + (c < FL ? 1 : 0);
+      bucket = (le + 3) / 4 - 1;
+    } else {
+#pragma unroll
+      for (int i = 0; i < FL; ++i) {
+        cr[i] = row(i);
+        c += id[i] != 0;
+      }
+      bucket = NBK - 1;
+    }
+    allpad = c == 0;
+    tt.cnt[s] = (uint8_t)(compact ? c : FL);
+    tt.pad_title[s] = allpad ? 1 : 0;
+    if (dedupe && allpad) bucket = -1;
   }
-  const uint64_t real = __ballot(any != 0);
-  const int64_t g = s >> 2;
-  const bool lead = (lane & 3) == 0 && g < n_groups;
-  const bool pad = ((real >> (lane & ~3)) & 0xFull) == 0;
-  if (lead) pad_group[g] = pad ? 1 : 0;
-  const uint64_t keep = __ballot(lead && !pad);
-  const uint64_t pads = __ballot(lead && pad);
-  if (lane == 0) {
-    wcount[w] = __popcll(keep);
-    wrep[w] = pads ? (int32_t)((s >> 2) + ((__ffsll((long long)pads) - 1) >> 2)) : INT32_MAX;
+  const uint64_t pads = __ballot(dedupe && allpad);
+  uint64_t bal[NBK];
+#pragma unroll
+  for (int b = 0; b < NBK; ++b) {
+    bal[b] = __ballot(bucket == b);
+    if (lane == 0) wcnt[b][w] = __popcll(bal[b]);
+  }
+  if (lane == 0) wrep[w] = pads ? (int32_t)((int64_t)blockIdx.x * CLS_T + 64 * w + __ffsll((long long)pads) - 1) : INT32_MAX;
+  __syncthreads();
+  if (threadIdx.x < NBK) {
+    const int b = threadIdx.x;
+    int tot = 0;
+    for (int i = 0; i < CLS_W; ++i) tot += wcnt[b][i];
+    int base = tot ? atomicAdd(&tt.counters[CNT_BUCKET + b], tot) : 0;
+    for (int i = 0; i < CLS_W; ++i) { wbase[b][i] = base; base += wcnt[b][i]; }
+  } else if (threadIdx.x == NBK) {
+    int r = INT32_MAX;
+    for (int i = 0; i < CLS_W; ++i) r = min(r, wrep[i]);
+    if (r != INT32_MAX) atomicMin(&tt.counters[CNT_REP], r);
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int r = INT32_MAX, tot = 0;
-    for (int i = 0; i < CLS_W; ++i) {
-      r = min(r, wrep[i]);
-      tot += wcount[i];
-    }
-    if (r != INT32_MAX) atomicMin(rep, r);
-    int b = tot ? atomicAdd(count, tot) : 0;
-    for (int i = 0; i < CLS_W; ++i) { wbase[i] = b; b += wcount[i]; }
-  }
-  __syncthreads();
-  if (lead && !pad) list[wbase[w] + __popcll(keep & ((1ull << lane) - 1))] = (int32_t)g;
+  uint64_t mine = 0;
+  int base = 0;
+#pragma unroll
+  for (int b = 0; b < NBK; ++b)
+    if (bucket == b) { mine = bal[b]; base = wbase[b][w]; }
+  if (bucket >= 0) tt.list[bucket * tt.stride + base + __popcll(mine & ((1ull << lane) - 1))] = (int32_t)s;
 }
 
-// out[s] = out[4 rep + s % 4] for every title s >= s0 of the other all-padding groups.
-__global__ __launch_bounds__(256) void broadcast_padding_kernel(const uint8_t* __restrict__ pad_group,
+// out[s] = out[rep] for every other all-padding title s >= s0.
+__global__ __launch_bounds__(256) void broadcast_padding_kernel(const uint8_t* __restrict__ pad_title,
                                                                 const int32_t* __restrict__ rep, int64_t s0,
                                                                 int64_t n_titles, float* __restrict__ out) {
   const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;   // (title - s0, float4 column)
   const int64_t s = s0 + t / (FD / 4);
-  if (s >= n_titles || !pad_group[s / FT]) return;
+  if (s >= n_titles || !pad_title[s]) return;
   const int64_t r = *rep;
-  if (s / FT == r) return;
+  if (s == r || r == INT32_MAX) return;
   const int c = (int)(t - (s - s0) * (FD / 4));
-  reinterpret_cast<float4*>(out + s * FD)[c] =
-      reinterpret_cast<const float4*>(out + (r * FT + (s % FT)) * FD)[c];
+  reinterpret_cast<float4*>(out + s * FD)[c] = reinterpret_cast<const float4*>(out + r * FD)[c];
 }
 
 // The clicked rows m < n_rows (titles 0 .. n_rows - 1 of the launch) whose
-// q|k|v the UserEncoder needs: all but the rows of all-padding groups other
-// than rep, whose news vectors are copies of rep's slot m % 4 (the UserEncoder
-// reads those rows from 4 rep + m % 4 instead). Appended in any order (vector
-// atomics, one per wave); the count must start at 0.
-// One 256-thread block lists rows m0 .. m0 + URL_ROWS - 1 (four 256-row
+// q|k|v the UserEncoder needs: all but the copied all-padding titles, whose
+// news vectors are rep's (the UserEncoder reads those rows from row rep).
+// Appended in any order (vector atomics, one per wave); the count must start
+// at 0. One 256-thread block lists rows m0 .. m0 + URL_ROWS - 1 (four 256-row
 // chunks), with one atomic (per-wave atomics on the one counter serialised:
 // 11 us; one per 256 rows: ~200 at config 3).
 constexpr int URL_ROWS = 1024, URL_C = URL_ROWS / 256;
-__device__ __forceinline__ void user_row_list_block(const uint8_t* __restrict__ pad_group,
+__device__ __forceinline__ void user_row_list_block(const uint8_t* __restrict__ pad_title,
                                                     const int32_t* __restrict__ rep, int64_t n_rows,
                                                     int64_t* __restrict__ list, int32_t* __restrict__ count,
                                                     int64_t m0) {
@@ -281,8 +340,8 @@ __device__ __forceinline__ void user_row_list_block(const uint8_t* __restrict__ 
   uint64_t ballot[URL_C];
 #pragma unroll
   for (int c = 0; c < URL_C; ++c) {
-    const int64_t m = m0 + 256 * c + threadIdx.x, g = m >> 2;
-    keep[c] = m < n_rows && !(pad_group[g] && g != r);
+    const int64_t m = m0 + 256 * c + threadIdx.x;
+    keep[c] = m < n_rows && !(pad_title[m] && m != r);
     ballot[c] = __ballot(keep[c]);
     if (lane == 0) wcount[4 * c + w] = __popcll(ballot[c]);
   }
@@ -299,11 +358,11 @@ __device__ __forceinline__ void user_row_list_block(const uint8_t* __restrict__ 
     if (keep[c]) list[wbase[4 * c + w] + __popcll(ballot[c] & ((1ull << lane) - 1))] = m0 + 256 * c + threadIdx.x;
 }
 
-__global__ __launch_bounds__(256) void user_row_list_kernel(const uint8_t* __restrict__ pad_group,
+__global__ __launch_bounds__(256) void user_row_list_kernel(const uint8_t* __restrict__ pad_title,
                                                             const int32_t* __restrict__ rep,
                                                             int64_t n_rows, int64_t* __restrict__ list,
                                                             int32_t* __restrict__ count) {
-  user_row_list_block(pad_group, rep, n_rows, list, count, (int64_t)blockIdx.x * URL_ROWS);
+  user_row_list_block(pad_title, rep, n_rows, list, count, (int64_t)blockIdx.x * URL_ROWS);
 }
 
 // The UserEncoder's row list, built by the deduplicating main pass itself
@@ -311,21 +370,34 @@ __global__ __launch_bounds__(256) void user_row_list_kernel(const uint8_t* __res
 struct UserRows {
   int64_t* list;   // null: not built here
   int64_t n_rows;
-  const uint8_t* pad_group;
+  const uint8_t* pad_title;
   const int32_t* rep;
   int32_t* count;
 };
 
-// Rows near fp32 overflow (nrms_common.hpp, kExpRecheck). The main pass
-// (EXACT = false) takes the fast exp everywhere and appends the title groups
-// that need the reference's exp to `list` (one entry per flagging wave;
-// duplicates are harmless: the recomputation is idempotent). A second launch
-// of the same kernel (EXACT = true) walks that list with the reference's exp
-// in every row and overwrites those groups' outputs. With no such rows (all
+// Titles near fp32 overflow (nrms_common.hpp, kExpRecheck). The main pass
+// (EXACT = false) takes the fast exp everywhere and appends (group << 4 |
+// title mask) for the titles that need the reference's exp (one entry per
+// flagging wave; duplicates are harmless: the recomputation is idempotent). A
+// second launch of the same kernel (EXACT = true) recomputes those groups with
+// the reference's exp in every row and overwrites the flagged titles' outputs
+// only (a title's result never depends on its group). With no such rows (all
 // real inputs), the second launch reads the zero count and exits.
 struct RecheckList {
   int32_t* count;
-  int32_t* list;   // capacity 4 * n_groups
+  int32_t* list;   // capacity 4 * (groups)
+};
+
+// The bucket lists as the main kernel reads them; list == null: no
+// classification (every title one 20-row slot, group k = titles 4k .. 4k + 3,
+// rows from the RowMap).
+struct TitleSet {
+  const int32_t* crow;
+  const uint8_t* cnt;
+  const int32_t* list;
+  const int32_t* counters;
+  int64_t stride;
+  int rep_bucket;   // the bucket rep is appended to (0 with compaction: Le = 1)
 };
 
 // Float offsets, within one q|k|v row, of what lane (head slot hl, x) of wave
@@ -348,7 +420,7 @@ __device__ __forceinline__ const NRMS_GLOBAL T* gptr(const float* p) {
   return reinterpret_cast<const NRMS_GLOBAL T*>(reinterpret_cast<uintptr_t>(p));
 }
 
-// Phase timing (profiles/probes/fused_timing.hip builds with NRMS_FUSED_TIMING):
+// Phase timing (profiles/probes/news_variants.hip builds with NRMS_FUSED_TIMING):
 // shader-cycle stamps accumulated per wave into dbg[wave][8].
 #ifdef NRMS_FUSED_TIMING
 #define NRMS_TIMING_PARAM , unsigned long long* __restrict__ dbg
@@ -397,9 +469,11 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 // MODE 0: f32 MFMA additive GEMM, fp32 context tile. MODE 1: split-bf16 x6,
 // context stored as bf16 planes. MODE 2: split-f16 x3 (main pass only; its
 // recheck pass runs MODE 1), context stored as fp16 planes.
+// A group of bucket NB holds 4 titles of LR = 4 NB rows each: title t's
+// compacted row p is tile row LR t + p (M = 16 NB rows, NB M-tiles).
 template <int MODE, bool EXACT>
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
-    const float* __restrict__ qkv, int64_t ldq, RowMap rmap, GroupList gl,
+    const float* __restrict__ qkv, int64_t ldq, RowMap rmap, TitleSet ts,
     const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
     RecheckList rl, UserRows ur NRMS_TIMING_PARAM) {
@@ -410,7 +484,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   if constexpr (!EXACT) {
     if (ur.list)   // (workgroup-uniform; the padding classification ran in an earlier launch)
       for (int64_t m0 = (int64_t)blockIdx.x * URL_ROWS; m0 < ur.n_rows; m0 += (int64_t)gridDim.x * URL_ROWS) {
-        user_row_list_block(ur.pad_group, ur.rep, ur.n_rows, ur.list, ur.count, m0);
+        user_row_list_block(ur.pad_title, ur.rep, ur.n_rows, ur.list, ur.count, m0);
         __syncthreads();   // (the block's LDS counters are reused)
       }
   }
@@ -418,8 +492,10 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   float* ctxL = lds;                                   // f32: [80][SC]
   __bf16* ctxB = reinterpret_cast<__bf16*>(lds);       // x6:  [80][XRB] = hi | mid | lo planes
   _Float16* ctxH = reinterpret_cast<_Float16*>(lds);   // f16x3: [80][XRH] = hi | lo planes
-  float* part = X6 ? lds + FROWS * XRB / 2 : (H3 ? lds + FROWS * XRH / 2 : ctxL + FROWS * SC);   // [80][4] per-wave row partials
-  const float** rowptr = reinterpret_cast<const float**>(part + 4 * FROWS);   // [2][80]
+  float* part = X6 ? lds + FROWS * XRB / 2 : (H3 ? lds + FROWS * XRH / 2 : ctxL + FROWS * SC);   // [80][8] row partials
+  const float** rowptr = reinterpret_cast<const float**>(part + PART_STRIDE * FROWS);   // [2][4 titles][20 slots]
+  int32_t* tmeta = reinterpret_cast<int32_t*>(rowptr + 2 * FROWS);   // [2][title index x4 | count x4]
+  int32_t* sched = tmeta + 16;   // [gend x NBK | bucket counts x NBK | rep | groups] (see below)
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float* zero_row = WaP + WAP_MAX;
@@ -444,37 +520,92 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     }
   }
 
-  // row pointers of title group tg -> rowptr[buf]: the token id is loaded by
-  // row_of (threads < 80), the pointer stored later by store_row, so the id
-  // load's latency hides behind the work in between.
-  const int64_t n_groups = (rmap.n_titles + FT - 1) / FT;
-  // row_of issues the id load unconditionally (a safe address where there is
-  // no id) and returns the raw value; store_row, at the end of phase A,
-  // recomputes the title / token from tg and maps it (out of range: NaN row,
-  // past the titles: zero row) — a use or a branch right after the load made
-  // the wait for it land at the start of the phase
-  auto tok = [&](int64_t tg, int64_t& s_, int& i_) __attribute__((always_inline)) -> bool {
-    int tl = tid;
-    asm volatile("" : "+v"(tl));   // (recomputed: a hoisted 64-bit token index spilled)
-    const int t = tl / FL;
-    i_ = tl - t * FL;
-    s_ = tg * FT + t;
-    return tl < FROWS && s_ < rmap.n_titles;
+  // ---- group schedule (workgroup-uniform, kept in LDS: as registers the
+  // five-bucket state spilled). Buckets NB = 5 .. 1 in turn (longest titles
+  // first, for the persistent loop's balance); gend[b] = one past the
+  // bucket's last group in that order.
+  const int64_t n_titles = rmap.n_titles;
+  if (tid == 0) {
+    int32_t n_groups = (int32_t)((n_titles + FT - 1) / FT);   // (groups < 2^27, checked at launch)
+    int32_t rep = INT32_MAX;
+    if (ts.list) {
+      rep = ts.counters[CNT_REP];
+      int32_t acc = 0;
+      for (int b = NBK - 1; b >= 0; --b) {
+        const int32_t cb = ts.counters[CNT_BUCKET + b];
+        const int32_t c = cb + ((b == ts.rep_bucket && rep != INT32_MAX) ? 1 : 0);
+        acc += (c + FT - 1) / FT;
+        sched[b] = acc;
+        sched[NBK + b] = cb;
+      }
+      n_groups = acc;
+    } else {
+      for (int b = 0; b < NBK; ++b) { sched[b] = n_groups; sched[NBK + b] = 0; }
+    }
+    sched[2 * NBK] = rep;
+    sched[2 * NBK + 1] = n_groups;
+  }
+  __syncthreads();
+  const int32_t n_groups = __builtin_amdgcn_readfirstlane(sched[2 * NBK + 1]);
+  // group k -> bucket (-1 past the end) and the group's index g within it
+  auto bucket_of = [&](int64_t k, int64_t& g) -> int {
+    int bsel = -1;
+    int32_t start = 0, prev = 0;
+#pragma unroll
+    for (int b = NBK - 1; b >= 0; --b) {
+      const int32_t ge = sched[b];
+      if (bsel < 0 && k < ge) { bsel = b; start = prev; }
+      prev = ge;
+    }
+    g = k - __builtin_amdgcn_readfirstlane(start);
+    return __builtin_amdgcn_readfirstlane(bsel);
   };
-  auto row_of = [&](int64_t tg) -> int64_t {
-    int64_t s_;
-    int i_;
-    const bool ok = tok(tg, s_, i_) && rmap.ids_a;
-    const int64_t* ip = ok ? rmap.ids_of(s_) + i_ : reinterpret_cast<const int64_t*>(WaP);
-    return *ip;
+  // title of slot t of group g of bucket b (-1: none)
+  auto title_of = [&](int b, int64_t g, int t) -> int32_t {
+    const int64_t c = FT * g + t;
+    if (!ts.list) return c < n_titles ? (int32_t)c : -1;   // (n_titles <= INT32_MAX, checked at launch)
+    const int32_t cbb = sched[NBK + b], rep = sched[2 * NBK];
+    if (c < cbb) return ts.list[b * ts.stride + c];
+    if (b == ts.rep_bucket && c == cbb && rep != INT32_MAX) return rep;
+    return -1;
   };
-  auto store_row = [&](int64_t raw, int64_t tg, int buf) {
-    int64_t s_;
-    int i_;
-    const bool ok = tok(tg, s_, i_);
-    const int64_t r = rmap.ids_a ? raw : s_ * FL + i_;
-    if (tid < FROWS)
-      rowptr[buf * FROWS + tid] = !ok ? zero_row : ((uint64_t)r < (uint64_t)rmap.n_rows ? qkv + r * ldq : nan_row);
+  // iteration idx: the group key k and (recheck pass) the mask of titles to write
+  const int64_t n_iter = EXACT ? (int64_t)*rl.count : n_groups;
+  auto key_at = [&](int64_t idx, int& tmask) -> int64_t {
+    tmask = 0xF;
+    if constexpr (EXACT) {
+      if (idx >= n_iter) return n_groups;
+      const int32_t e = rl.list[idx];
+      tmask = e & 0xF;
+      return (int64_t)(e >> 4);
+    }
+    return idx;
+  };
+
+  // Row pointers of a group: slot (t = tid / 20, p = tid % 20) of threads
+  // tid < 80, in three stages so that the dependent loads (bucket list ->
+  // compacted row id) hide behind the attention phase: title index, then its
+  // row id and count, then the pointer and the title's (index, count) into LDS.
+  const int tslot = tid / FL, pslot = tid - tslot * FL;
+  auto stage1 = [&](int b, int64_t g) -> int32_t { return (tid < FROWS && b >= 0) ? title_of(b, g, tslot) : -1; };
+  auto stage2 = [&](int32_t s, int& c) -> int64_t {
+    c = 0;
+    if (s < 0) return -2;
+    if (ts.crow) {
+      c = ts.cnt[s];
+      return (int64_t)ts.crow[(int64_t)s * FL + pslot];
+    }
+    c = FL;
+    return rmap(s, pslot);
+  };
+  auto stage3 = [&](int32_t s, int64_t r, int c, int buf) {
+    if (tid < FROWS) {
+      rowptr[buf * FROWS + tid] = r == -2 ? zero_row : (r < 0 ? nan_row : qkv + r * ldq);
+      if (pslot == 0) {
+        tmeta[8 * buf + tslot] = s;
+        tmeta[8 * buf + 4 + tslot] = c;
+      }
+    }
   };
 
   // attention roles: block b = (title t, head slot hl), lane x within the block
@@ -504,7 +635,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   const float* Aw = ctxL + lm * SC + 4 * kq;
 
   // q|k|v slices of one title group, lane (block (t, hl), x): Q / K of tokens
-  // x + 4j, V dims 5x..5x+4 of all 20 tokens. Loaded for the NEXT group: Q / K
+  // x + 4j, V dims 5x..5x+4 of tokens k < 4 NB. Loaded for the NEXT group: Q / K
   // at the start of the B epilogue (in flight behind the tanh work, a barrier
   // and the pooling), V at the end of C (behind the next S^T phase).
   float qf[5][FDK], kf[5][FDK], vf[FL][5];
@@ -518,9 +649,18 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       kf[j][4 * c] = b.x; kf[j][4 * c + 1] = b.y; kf[j][4 * c + 2] = b.z; kf[j][4 * c + 3] = b.w;
     }
   };
-  auto prefetch_qk = [&](int buf) {
+  // slices past the next group's rows are zeroed, not left alone: a register
+  // the next group might read is live across the GEMM otherwise (spills)
+  auto zero_qk_tok = [&](int j) {
 #pragma unroll
-    for (int j = 0; j < 5; ++j) prefetch_qk_tok(buf, j);
+    for (int d = 0; d < FDK; ++d) { qf[j][d] = 0.f; kf[j][d] = 0.f; }
+  };
+  auto prefetch_qk = [&](int buf, int nbq) {
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      if (j < nbq) prefetch_qk_tok(buf, j);
+      else zero_qk_tok(j);
+    }
   };
   // (50 + 40 loads in two batches: at most 63 may be outstanding per wave)
   auto prefetch_v_tok = [&](int buf, int k) {
@@ -529,28 +669,34 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     vf[k][0] = a.x; vf[k][1] = a.y; vf[k][2] = a.z; vf[k][3] = a.w;
     vf[k][4] = *gptr<float>(vr + Off::v1(w, hls, x));
   };
-  auto prefetch_v = [&](int buf) {
+  auto prefetch_v = [&](int buf, int nbq) {
 #pragma unroll
-    for (int k = 0; k < FL; ++k) prefetch_v_tok(buf, k);
+    for (int kb = 0; kb < 5; ++kb) {
+      if (kb < nbq) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) prefetch_v_tok(buf, 4 * kb + r);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int m = 0; m < 5; ++m) vf[4 * kb + r][m] = 0.f;
+      }
+    }
   };
 
-  // iteration k of this workgroup handles title group group_at(k): k itself in
-  // the main pass, the k-th flagged group in the EXACT pass (past the end: a
-  // group of padding titles, so the prefetch of "the next group" stays valid)
-  // (main pass with a group list: the listed groups, then rep)
-  const int64_t n_list = gl.list ? (int64_t)*gl.count : n_groups;
-  const int32_t rep = gl.list ? *gl.rep : INT32_MAX;
-  const int64_t n_iter = EXACT ? (int64_t)*rl.count : n_list + (rep != INT32_MAX ? 1 : 0);
-  auto group_at = [&](int64_t k) -> int64_t {
-    if constexpr (EXACT) return k < n_iter ? (int64_t)rl.list[k] : n_groups;
-    if (gl.list) return k < n_list ? (int64_t)gl.list[k] : (k == n_list && rep != INT32_MAX ? (int64_t)rep : n_groups);
-    else return k;
-  };
-  if (blockIdx.x < n_iter) store_row(row_of(group_at(blockIdx.x)), group_at(blockIdx.x), 0);
-  __syncthreads();
-  if (blockIdx.x < n_iter) {
-    prefetch_qk(0);
-    prefetch_v(0);
+  {
+    int tm0;
+    int64_t g0 = 0;
+    const int b0 = (int64_t)blockIdx.x < n_iter ? bucket_of(key_at(blockIdx.x, tm0), g0) : -1;
+    int c0;
+    const int32_t s0 = stage1(b0, g0);
+    const int64_t r0 = stage2(s0, c0);
+    stage3(s0, r0, c0, 0);
+    __syncthreads();
+    if (b0 >= 0) {
+      prefetch_qk(0, b0 + 1);
+      prefetch_v(0, b0 + 1);
+    }
   }
 #ifdef NRMS_FUSED_TIMING
   unsigned long long tacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -558,397 +704,486 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #endif
 
   int it = 0;
-  for (int64_t k = blockIdx.x; k < n_iter; k += gridDim.x, ++it) {
-    const int64_t tg = group_at(k);
-    const int nbuf = (it + 1) & 1;
-    // (no barrier here: the context tile's last readers, the previous group's
-    // B mainloop, finished before its B -> C barrier; C reads registers + part)
+  // one iteration: group key_at(idx), of bucket NB - 1
+  auto iterate = [&](int64_t idx, auto nbc) {
+    constexpr int NB = decltype(nbc)::value;
+    int tmask, tmask_n;
+    const int64_t k = key_at(idx, tmask);
+    int64_t g, gn = 0;
+    bucket_of(k, g);
+    const int64_t kn = key_at(idx + gridDim.x, tmask_n);
+    const int bn = (idx + gridDim.x < n_iter) ? bucket_of(kn, gn) : -1;
+    const int nb_next = bn + 1;   // 0: no next group
+    const int buf = it & 1, nbuf = buf ^ 1;
+    {
+      // this lane's title's real-token count (its index is read in C)
+      const int my_c = tmeta[8 * buf + 4 + at];
+      constexpr int LR = 4 * NB;             // tile rows per title
+      constexpr int XMAX = 23 - 4 * NB;      // most extra additions of the rep's exp (n_pad - 1)
+      // compacted length Le = c + (c < 20) in [LR - 3, LR]; the rep (row c,
+      // multiplicity n_pad = 20 - c) sits in the last key block, register rrep
+      const int le = my_c + (my_c < FL ? 1 : 0);
+      const int npad = FL - my_c;
+      const int rrep = my_c - 4 * (NB - 1);
+      // (no barrier here: the context tile's last readers, the previous group's
+      // B mainloop, finished before its B -> C barrier; C reads registers + part)
 #ifdef NRMS_FUSED_TIMING
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // probe only: time the wait for this group's q|k|v
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // probe only: time the wait for this group's q|k|v
 #endif
-    NRMS_STAMP(0)
-    floatx4 O[5][5];   // this wave's context rows, live until the pooling in C
-    uint64_t recheck = 0;   // lanes whose row needs the recheck pass (RecheckList)
+      NRMS_STAMP(0)
+      floatx4 O[5][NB];   // this wave's context rows, live until the pooling in C
+      uint64_t recheck = 0;   // lanes whose row needs the recheck pass (RecheckList)
 
-    // ---------------- A: attention (4x4x1 MFMA, 16 (title, head) blocks) --------------
-    {
-      // row pointers of the next group, for the prefetch in this group's B
-      // epilogue (past the last group: zero rows, so the prefetch is
-      // unconditional and its registers are dead during the GEMM); stored at
-      // the end of this phase
-      const int64_t next_tg = group_at(k + gridDim.x);
-      const int64_t next_row = row_of(next_tg);
-      // S^T tiles: rows = keys 4j + r (A = K), cols = queries 4i + x (B = Q)
-      floatx4 S[5][5];
+      // ---------------- A: attention (4x4x1 MFMA, 16 (title, head) blocks) --------------
+      {
+        // the next group's slot rows (stage 1 now, stage 2 after the first
+        // query column, stored at the end of this phase for the prefetch in
+        // this group's B epilogue)
+        const int32_t s_next = stage1(bn, gn);
+        int c_next = 0;
+        int64_t r_next = -2;
+        // S^T tiles: rows = keys 4j + r (A = K), cols = queries 4i + x (B = Q)
+        floatx4 S[NB][NB];
 #pragma unroll
-      for (int j = 0; j < 5; ++j)
+        for (int j = 0; j < NB; ++j)
 #pragma unroll
-        for (int i = 0; i < 5; ++i) S[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-      // One query column i at a time (S^T, exp, ctx^T, split + store), so a
-      // column's S registers die before the next column's are written: short
-      // live ranges, no spills (all S^T first, then all ctx^T: 2 % slower;
-      // column i's split interleaved with column i + 1's MFMAs through
-      // sched_group_barrier: no better).
-      auto s_mfma = [&](int i) {
+          for (int i = 0; i < NB; ++i) S[j][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+        // One query column i at a time (S^T, exp, ctx^T, split + store), so a
+        // column's S registers die before the next column's are written: short
+        // live ranges, no spills.
+        auto s_mfma = [&](int i) {
 #pragma unroll
-        for (int d = 0; d < FDK; ++d)
+          for (int d = 0; d < FDK; ++d)
 #pragma unroll
-          for (int j = 0; j < 5; ++j) S[j][i] = mfma4(kf[j][d], qf[i][d], S[j][i]);
-      };
-      // P = exp(S / sqrt(dk)) / (sum_keys + 1e-8): query 4i + x, key 4j + r
-      auto s_exp = [&](int i) {
-        float sum = 0.f;
-#pragma unroll
-        for (int j = 0; j < 5; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float e = EXACT ? ref_exp(S[j][i][r], sqrt_dk)
-                                  : __builtin_amdgcn_exp2f(S[j][i][r] * c_exp);
-            S[j][i][r] = e;
-            sum += e;
-          }
-        // rows near fp32 overflow (or non-finite): flagged (no branch here),
-        // recomputed by the EXACT pass (RecheckList)
-        if constexpr (!EXACT) recheck |= __builtin_amdgcn_ballot_w64(exp_row_needs_recheck(sum));
-        const float inv = 1.0f / (sum + 1e-8f);
-#pragma unroll
-        for (int j = 0; j < 5; ++j)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) S[j][i][r] *= inv;
-      };
-      // ctx^T tiles: rows = dims 5r' + m (A = V^T), cols = queries 4i + x (B = P^T);
-      // lane x holds ctx[query 4i + x][dim 5r' + m] = O[m][i][r']
-      auto o_mfma = [&](int i) {
-#pragma unroll
-        for (int m = 0; m < 5; ++m) O[m][i] = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int k = 0; k < FL; ++k)
-#pragma unroll
-          for (int m = 0; m < 5; ++m) O[m][i] = mfma4(vf[k][m], S[k >> 2][i][k & 3], O[m][i]);
-      };
-      // (a branch-free form, with the idle head slot storing its bit-identical
-      // copy of head 12, measured 9 % slower: the compiler then interleaves the
-      // stores into the next column's MFMAs and spills)
-      auto o_store = [&](int i) {
-        if (!hval) return;
-        if constexpr (H3) {
-          _Float16* dst = ctxH + (FL * at + 4 * i + x) * XRH + FDK * h;
-#pragma unroll
-          for (int c = 0; c < FDK / 4; ++c) {
-            uint32_t hw[2], lw[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int d = 4 * c + 2 * e;
-              split2x2h(O[d % 5][i][d / 5], O[(d + 1) % 5][i][(d + 1) / 5], hw[e], lw[e]);
-            }
-            *reinterpret_cast<uint2*>(dst + 4 * c) = make_uint2(hw[0], hw[1]);
-            *reinterpret_cast<uint2*>(dst + XKP + 4 * c) = make_uint2(lw[0], lw[1]);
-          }
-        } else if constexpr (X6) {
-          __bf16* dst = ctxB + (FL * at + 4 * i + x) * XRB + FDK * h;
-#pragma unroll
-          for (int c = 0; c < FDK / 4; ++c) {
-            uint32_t h[2], m[2], l[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int d = 4 * c + 2 * e;
-              split3x2(O[d % 5][i][d / 5], O[(d + 1) % 5][i][(d + 1) / 5], h[e], m[e], l[e]);
-            }
-            *reinterpret_cast<uint2*>(dst + 4 * c) = make_uint2(h[0], h[1]);
-            *reinterpret_cast<uint2*>(dst + XKP + 4 * c) = make_uint2(m[0], m[1]);
-            *reinterpret_cast<uint2*>(dst + 2 * XKP + 4 * c) = make_uint2(l[0], l[1]);
-          }
-        } else {
-          float4* dst = reinterpret_cast<float4*>(ctxL + (FL * at + 4 * i + x) * SC + FDK * h);
-#pragma unroll
-          for (int c = 0; c < FDK / 4; ++c) {
-            const int d0 = 4 * c;
-            dst[c] = make_float4(O[d0 % 5][i][d0 / 5], O[(d0 + 1) % 5][i][(d0 + 1) / 5],
-                                 O[(d0 + 2) % 5][i][(d0 + 2) / 5], O[(d0 + 3) % 5][i][(d0 + 3) / 5]);
-          }
-        }
-      };
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        s_mfma(i);
-        s_exp(i);
-        o_mfma(i);
-        o_store(i);
-      }
-      store_row(next_row, next_tg, nbuf);
-    }
-    NRMS_STAMP(1)
-    __syncthreads();   // context tile complete
-    NRMS_STAMP(2)
-
-    // ---------------- B: additive GEMM + tanh·q row partials ----------------
-    {
-      floatx4 acc[FMT][3], accX = floatx4{0.f, 0.f, 0.f, 0.f}, accX2 = floatx4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int mt = 0; mt < FMT; ++mt)
-#pragma unroll
-        for (int j = 0; j < 3; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
-      if constexpr (X6) {
-        // A fragments (16x16x32): lane holds A[row lm][32 ks + 8 kq .. + 7] of each plane
-        const __bf16* Ab = ctxB + lm * XRB + 8 * kq;
-        // B fragments through a buffer resource (as the F16X3 path below)
-        const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(WaP), 0, WAP3_FLOATS * 4, 0x00020000);
-        int bvoff[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) bvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
-        // plane-major: the hi planes (first product's B) arrive first
-        auto load_b = [&](int ks, bf16x8 (&dst)[4][3]) {
-#pragma unroll
-          for (int pl = 0; pl < 3; ++pl)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              dst[j][pl] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                  brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
+            for (int j = 0; j < NB; ++j) S[j][i] = mfma4(kf[j][d], qf[i][d], S[j][i]);
         };
-        // one 32-deep k-step; EXTRA: wave 0 also owns (M-tile 4, N-tile 12)
-        // the wave index is a template constant (the X tile's A rows = M-tile
-        // W: no second read of them); A planes loaded lo first, the order the
-        // products consume them
-        auto kstep = [&](int ks, const bf16x8 (&bb)[4][3], auto wc) {
-          constexpr int W = decltype(wc)::value;
-          constexpr bool EXTRA = W == 0;
-          bf16x8 a[FMT][3];
+        // P = exp(S / sqrt(dk)) / (sum_keys + 1e-8): query 4i + x, key 4j + r.
+        // Keys past Le (unused slots) are 0; the rep's other n_pad - 1 copies
+        // are added after the rep, one at a time (the uncompacted sum, bitwise).
+        auto s_exp = [&](int i) {
+          float sum = 0.f;
 #pragma unroll
-          for (int pl = 2; pl >= 0; --pl)
+          for (int j = 0; j < NB; ++j)
 #pragma unroll
-            for (int mt = 0; mt < FMT; ++mt)
-              a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * XRB + pl * XKP + 32 * ks);
-          const bf16x8 (&ax)[3] = a[W];
-          // the six products with i + j <= 2, smallest first
+            for (int r = 0; r < 4; ++r) {
+              float e = EXACT ? ref_exp(S[j][i][r], sqrt_dk) : __builtin_amdgcn_exp2f(S[j][i][r] * c_exp);
+              if (j == NB - 1) e = (4 * j + r < le) ? e : 0.f;
+              S[j][i][r] = e;
+              sum += e;
+            }
+          float erep = 0.f;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) erep = r == rrep ? S[NB - 1][i][r] : erep;
+#pragma unroll
+          for (int c = 0; c < XMAX; ++c) sum += (c + 1 < npad) ? erep : 0.f;
+          // rows near fp32 overflow (or non-finite): flagged (no branch here),
+          // recomputed by the EXACT pass (RecheckList)
+          if constexpr (!EXACT) recheck |= __builtin_amdgcn_ballot_w64(exp_row_needs_recheck(sum));
+          const float inv = 1.0f / (sum + 1e-8f);
+#pragma unroll
+          for (int j = 0; j < NB; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) S[j][i][r] *= inv;
+          // the rep key's weight carries its multiplicity into ctx = sum_k P_k v_k
+          const float fpad = (float)npad;
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            S[NB - 1][i][r] = (r == rrep && npad > 1) ? S[NB - 1][i][r] * fpad : S[NB - 1][i][r];
+        };
+        // ctx^T tiles: rows = dims 5r' + m (A = V^T), cols = queries 4i + x (B = P^T);
+        // lane x holds ctx[query 4i + x][dim 5r' + m] = O[m][i][r']
+        auto o_mfma = [&](int i) {
+#pragma unroll
+          for (int m = 0; m < 5; ++m) O[m][i] = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kk = 0; kk < LR; ++kk)
+#pragma unroll
+            for (int m = 0; m < 5; ++m) O[m][i] = mfma4(vf[kk][m], S[kk >> 2][i][kk & 3], O[m][i]);
+        };
+        // (a branch-free form, with the idle head slot storing its bit-identical
+        // copy of head 12, measured 9 % slower: the compiler then interleaves the
+        // stores into the next column's MFMAs and spills)
+        auto o_store = [&](int i) {
+          if (!hval) return;
+          const int row = LR * at + 4 * i + x;
+          if constexpr (H3) {
+            _Float16* dst = ctxH + row * XRH + FDK * h;
+#pragma unroll
+            for (int c = 0; c < FDK / 4; ++c) {
+              uint32_t hw[2], lw[2];
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                const int d = 4 * c + 2 * e;
+                split2x2h(O[d % 5][i][d / 5], O[(d + 1) % 5][i][(d + 1) / 5], hw[e], lw[e]);
+              }
+              *reinterpret_cast<uint2*>(dst + 4 * c) = make_uint2(hw[0], hw[1]);
+              *reinterpret_cast<uint2*>(dst + XKP + 4 * c) = make_uint2(lw[0], lw[1]);
+            }
+          } else if constexpr (X6) {
+            __bf16* dst = ctxB + row * XRB + FDK * h;
+#pragma unroll
+            for (int c = 0; c < FDK / 4; ++c) {
+              uint32_t hh[2], m[2], l[2];
+#pragma unroll
+              for (int e = 0; e < 2; ++e) {
+                const int d = 4 * c + 2 * e;
+                split3x2(O[d % 5][i][d / 5], O[(d + 1) % 5][i][(d + 1) / 5], hh[e], m[e], l[e]);
+              }
+              *reinterpret_cast<uint2*>(dst + 4 * c) = make_uint2(hh[0], hh[1]);
+              *reinterpret_cast<uint2*>(dst + XKP + 4 * c) = make_uint2(m[0], m[1]);
+              *reinterpret_cast<uint2*>(dst + 2 * XKP + 4 * c) = make_uint2(l[0], l[1]);
+            }
+          } else {
+            float4* dst = reinterpret_cast<float4*>(ctxL + row * SC + FDK * h);
+#pragma unroll
+            for (int c = 0; c < FDK / 4; ++c) {
+              const int d0 = 4 * c;
+              dst[c] = make_float4(O[d0 % 5][i][d0 / 5], O[(d0 + 1) % 5][i][(d0 + 1) / 5],
+                                   O[(d0 + 2) % 5][i][(d0 + 2) / 5], O[(d0 + 3) % 5][i][(d0 + 3) / 5]);
+            }
+          }
+        };
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          s_mfma(i);
+          s_exp(i);
+          o_mfma(i);
+          o_store(i);
+          if (i == 0) r_next = stage2(s_next, c_next);
+        }
+        stage3(s_next, r_next, c_next, nbuf);
+      }
+      NRMS_STAMP(1)
+      __syncthreads();   // context tile complete
+      NRMS_STAMP(2)
+
+      // ---------------- B: additive GEMM + tanh·q row partials ----------------
+      // Wave w: N-tiles 3w..3w+2 of every M-tile, and N-tile 12 (the last, half
+      // past Q) of M-tile w (w < NB) and, for wave 0, of M-tile 4 (NB = 5). Each
+      // row's score sums its partials in one order, (((p0 + p1) + p2) + p3) + p12,
+      // whichever wave holds N-tile 12 for it: a title's result does not depend
+      // on its slot.
+      {
+        floatx4 acc[NB][3], accX = floatx4{0.f, 0.f, 0.f, 0.f}, accX2 = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int mt = 0; mt < NB; ++mt)
+#pragma unroll
+          for (int j = 0; j < 3; ++j) acc[mt][j] = floatx4{0.f, 0.f, 0.f, 0.f};
+        if constexpr (X6) {
+          // A fragments (16x16x32): lane holds A[row lm][32 ks + 8 kq .. + 7] of each plane
+          const __bf16* Ab = ctxB + lm * XRB + 8 * kq;
+          const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<float*>(WaP), 0, WAP3_FLOATS * 4, 0x00020000);
+          int bvoff[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) bvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
+          // plane-major: the hi planes (first product's B) arrive first
+          auto load_b = [&](int ks, bf16x8 (&dst)[4][3]) {
+#pragma unroll
+            for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+              for (int j = 0; j < 4; ++j)
+                dst[j][pl] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                    brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
+          };
+          // one 32-deep k-step; the wave index is a template constant (its N-tile
+          // 12 rows = M-tile W: no second read of them); A planes loaded lo
+          // first, the order the products consume them
+          auto kstep = [&](int ks, const bf16x8 (&bb)[4][3], auto wc) {
+            constexpr int W = decltype(wc)::value;
+            constexpr bool HASX = W < NB;
+            constexpr bool EXTRA = W == 0 && NB == 5;
+            bf16x8 a[NB][3];
+#pragma unroll
+            for (int pl = 2; pl >= 0; --pl)
+#pragma unroll
+              for (int mt = 0; mt < NB; ++mt)
+                a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * XRB + pl * XKP + 32 * ks);
+            // the six products with i + j <= 2, smallest first
 #define NRMS_X6STEP(PA, PB)                                                                              \
-  _Pragma("unroll") for (int mt = 0; mt < FMT; ++mt)                                                     \
+  _Pragma("unroll") for (int mt = 0; mt < NB; ++mt)                                                      \
   _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                          \
       acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);   \
-  accX = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[PA], bb[3][PB], accX, 0, 0, 0);                      \
-  if constexpr (EXTRA) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[FMT - 1][PA], bb[3][PB], accX2, 0, 0, 0);
-          NRMS_X6STEP(2, 0) NRMS_X6STEP(1, 1) NRMS_X6STEP(0, 2) NRMS_X6STEP(1, 0) NRMS_X6STEP(0, 1)
-          NRMS_X6STEP(0, 0)
+  if constexpr (HASX) accX = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[HASX ? W : 0][PA], bb[3][PB], accX, 0, 0, 0); \
+  if constexpr (EXTRA) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
+            NRMS_X6STEP(2, 0) NRMS_X6STEP(1, 1) NRMS_X6STEP(0, 2) NRMS_X6STEP(1, 0) NRMS_X6STEP(0, 1)
+            NRMS_X6STEP(0, 0)
 #undef NRMS_X6STEP
-        };
-        // two B buffers in turn (XKS is even): no register copies between k-steps
-        auto mainloop = [&](auto extra) {
-          bf16x8 b0[4][3], b1[4][3];
-          load_b(0, b0);
+          };
+          // two B buffers in turn (XKS is even): no register copies between k-steps
+          auto mainloop = [&](auto wc) {
+            bf16x8 b0[4][3], b1[4][3];
+            load_b(0, b0);
 #pragma unroll
-          for (int ks = 0; ks < XKS; ks += 2) {
-            load_b(ks + 1, b1);
-            kstep(ks, b0, extra);
-            __builtin_amdgcn_sched_barrier(0);
-            if (ks + 2 < XKS) load_b(ks + 2, b0);
-            kstep(ks + 1, b1, extra);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int ks = 0; ks < XKS; ks += 2) {
+              load_b(ks + 1, b1);
+              kstep(ks, b0, wc);
+              __builtin_amdgcn_sched_barrier(0);
+              if (ks + 2 < XKS) load_b(ks + 2, b0);
+              kstep(ks + 1, b1, wc);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          };
+          static_assert(XKS % 2 == 0, "k-steps in pairs");
+          switch (w) {
+            case 0: mainloop(std::integral_constant<int, 0>{}); break;
+            case 1: mainloop(std::integral_constant<int, 1>{}); break;
+            case 2: mainloop(std::integral_constant<int, 2>{}); break;
+            default: mainloop(std::integral_constant<int, 3>{}); break;
           }
-        };
-        static_assert(XKS % 2 == 0, "k-steps in pairs");
-        switch (w) {
-          case 0: mainloop(std::integral_constant<int, 0>{}); break;
-          case 1: mainloop(std::integral_constant<int, 1>{}); break;
-          case 2: mainloop(std::integral_constant<int, 2>{}); break;
-          default: mainloop(std::integral_constant<int, 3>{}); break;
-        }
-      } else if constexpr (H3) {
-        // products lo·hi, hi·lo, hi·hi' (each 2^11 x the true product) into acc
-        const _Float16* Ah = ctxH + lm * XRH + 8 * kq;
-        // B fragments through a buffer resource: one VGPR offset (the lane), the
-        // fragment offset in an SGPR (no per-load address registers when unrolled)
-        const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
-            const_cast<float*>(WaP + WAP_MAX + SPECIAL_FLOATS), 0, WAP2_FLOATS * 4, 0x00020000);
-        int bvoff[4];   // lane + N-tile in the VGPR offset; k-step in soffset; plane immediate
+        } else if constexpr (H3) {
+          // products lo·hi, hi·lo, hi·hi' (each 2^11 x the true product) into acc
+          const _Float16* Ah = ctxH + lm * XRH + 8 * kq;
+          // B fragments through a buffer resource: one VGPR offset (the lane), the
+          // fragment offset in an SGPR (no per-load address registers when unrolled)
+          const __amdgpu_buffer_rsrc_t brs = __builtin_amdgcn_make_buffer_rsrc(
+              const_cast<float*>(WaP + WAP_MAX + SPECIAL_FLOATS), 0, WAP2_FLOATS * 4, 0x00020000);
+          int bvoff[4];   // lane + N-tile in the VGPR offset; k-step in soffset; plane immediate
 #pragma unroll
-        for (int j = 0; j < 4; ++j) bvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
-        // B plane pb: 0 = hi' (formed in registers from hi: 2,048 hi is exact,
-        // and the pack stores NaN in hi where it would pass fp16's range; the
-        // packed hi' plane is not read — 2/3 of the fragment loads: news_fused
-        // -2 %), 1 = lo, 2 = hi; loaded in consumption order
-        auto load_b = [&](int ks, f16x8 (&dst)[4][3]) {
+          for (int j = 0; j < 4; ++j) bvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
+          // B plane pb: 0 = hi' (formed in registers from hi: 2,048 hi is exact,
+          // and the pack stores NaN in hi where it would pass fp16's range; the
+          // packed hi' plane is not read), 1 = lo, 2 = hi; loaded in consumption order
+          auto load_b = [&](int ks, f16x8 (&dst)[4][3]) {
 #pragma unroll
-          for (int pl = 2; pl >= 1; --pl)
+            for (int pl = 2; pl >= 1; --pl)
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-              dst[j][pl] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(
-                  brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
-        };
-        auto kstep = [&](int ks, f16x8 (&bb)[4][3], auto wc) {
-          constexpr int W = decltype(wc)::value;
-          constexpr bool EXTRA = W == 0;
+              for (int j = 0; j < 4; ++j)
+                dst[j][pl] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(
+                    brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
+          };
+          auto kstep = [&](int ks, f16x8 (&bb)[4][3], auto wc) {
+            constexpr int W = decltype(wc)::value;
+            constexpr bool HASX = W < NB;
+            constexpr bool EXTRA = W == 0 && NB == 5;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) bb[j][0] = bb[j][2] * (_Float16)kF16LoScale;
-          f16x8 a[FMT][2];
+            for (int j = 0; j < 4; ++j) bb[j][0] = bb[j][2] * (_Float16)kF16LoScale;
+            f16x8 a[NB][2];
 #pragma unroll
-          for (int pl = 1; pl >= 0; --pl)
+            for (int pl = 1; pl >= 0; --pl)
 #pragma unroll
-            for (int mt = 0; mt < FMT; ++mt)
-              a[mt][pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * mt * XRH + pl * XKP + 32 * ks);
-          const f16x8 (&ax)[2] = a[W];
+              for (int mt = 0; mt < NB; ++mt)
+                a[mt][pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * mt * XRH + pl * XKP + 32 * ks);
 #define NRMS_H3STEP(PA, PB)                                                                            \
-  _Pragma("unroll") for (int mt = 0; mt < FMT; ++mt)                                                   \
+  _Pragma("unroll") for (int mt = 0; mt < NB; ++mt)                                                    \
   _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                        \
       acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);  \
-  accX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ax[PA], bb[3][PB], accX, 0, 0, 0);                     \
-  if constexpr (EXTRA) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[FMT - 1][PA], bb[3][PB], accX2, 0, 0, 0);
-          NRMS_H3STEP(1, 2) NRMS_H3STEP(0, 1) NRMS_H3STEP(0, 0)
+  if constexpr (HASX) accX = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[HASX ? W : 0][PA], bb[3][PB], accX, 0, 0, 0); \
+  if constexpr (EXTRA) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
+            NRMS_H3STEP(1, 2) NRMS_H3STEP(0, 1) NRMS_H3STEP(0, 0)
 #undef NRMS_H3STEP
-        };
-        auto mainloop = [&](auto extra) {
-          f16x8 b0[4][3], b1[4][3];
-          load_b(0, b0);
-          // fully unrolled, each k-step's loads and MFMAs fenced in place
-          // (without the fences the scheduler hoists every load: 1,100 spills);
-          // a rolled loop permuted the accumulators at its back-edge (~170
-          // AGPR moves per iteration): 1.41 -> 1.33 ms
+          };
+          auto mainloop = [&](auto wc) {
+            f16x8 b0[4][3], b1[4][3];
+            load_b(0, b0);
+            // fully unrolled, each k-step's loads and MFMAs fenced in place
+            // (without the fences the scheduler hoists every load: 1,100 spills);
+            // a rolled loop permuted the accumulators at its back-edge (~170
+            // AGPR moves per iteration): 1.41 -> 1.33 ms
 #pragma unroll
-          for (int ks = 0; ks < XKS; ks += 2) {
-            load_b(ks + 1, b1);
-            kstep(ks, b0, extra);
-            __builtin_amdgcn_sched_barrier(0);
-            if (ks + 2 < XKS) load_b(ks + 2, b0);
-            kstep(ks + 1, b1, extra);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int ks = 0; ks < XKS; ks += 2) {
+              load_b(ks + 1, b1);
+              kstep(ks, b0, wc);
+              __builtin_amdgcn_sched_barrier(0);
+              if (ks + 2 < XKS) load_b(ks + 2, b0);
+              kstep(ks + 1, b1, wc);
+              __builtin_amdgcn_sched_barrier(0);
+            }
+          };
+          switch (w) {
+            case 0: mainloop(std::integral_constant<int, 0>{}); break;
+            case 1: mainloop(std::integral_constant<int, 1>{}); break;
+            case 2: mainloop(std::integral_constant<int, 2>{}); break;
+            default: mainloop(std::integral_constant<int, 3>{}); break;
           }
-        };
-        switch (w) {
-          case 0: mainloop(std::integral_constant<int, 0>{}); break;
-          case 1: mainloop(std::integral_constant<int, 1>{}); break;
-          case 2: mainloop(std::integral_constant<int, 2>{}); break;
-          default: mainloop(std::integral_constant<int, 3>{}); break;
-        }
 #pragma unroll
-        for (int mt = 0; mt < FMT; ++mt)
+          for (int mt = 0; mt < NB; ++mt)
 #pragma unroll
-          for (int j = 0; j < 3; ++j) acc[mt][j] *= kLoUnscale;
-        accX *= kLoUnscale;
-        accX2 *= kLoUnscale;
-      } else {
-      float4 bb[4], bn[4];
+            for (int j = 0; j < 3; ++j) acc[mt][j] *= kLoUnscale;
+          accX *= kLoUnscale;
+          accX2 *= kLoUnscale;
+        } else {
+          float4 bb[4], bn4[4];
 #pragma unroll
-      for (int j = 0; j < 3; ++j) bb[j] = Bp[(3 * w + j) * 64];
-      bb[3] = Bp[12 * 64];
-      for (int c = 0; c < FKG; ++c) {
-        if (c + 1 < FKG) {
+          for (int j = 0; j < 3; ++j) bb[j] = Bp[(3 * w + j) * 64];
+          bb[3] = Bp[12 * 64];
+          for (int c = 0; c < FKG; ++c) {
+            if (c + 1 < FKG) {
 #pragma unroll
-          for (int j = 0; j < 3; ++j) bn[j] = Bp[((c + 1) * FNT + 3 * w + j) * 64];
-          bn[3] = Bp[((c + 1) * FNT + 12) * 64];
-        }
-        float4 a[FMT];
+              for (int j = 0; j < 3; ++j) bn4[j] = Bp[((c + 1) * FNT + 3 * w + j) * 64];
+              bn4[3] = Bp[((c + 1) * FNT + 12) * 64];
+            }
+            float4 a[NB];
 #pragma unroll
-        for (int mt = 0; mt < FMT; ++mt) a[mt] = *reinterpret_cast<const float4*>(Aw + 16 * mt * SC + 16 * c);
-        const float4 ax = *reinterpret_cast<const float4*>(Aw + 16 * w * SC + 16 * c);
+            for (int mt = 0; mt < NB; ++mt) a[mt] = *reinterpret_cast<const float4*>(Aw + 16 * mt * SC + 16 * c);
+            const float4 ax = *reinterpret_cast<const float4*>(Aw + 16 * (w < NB ? w : 0) * SC + 16 * c);
 #define NRMS_KSTEP(F)                                                                             \
-  _Pragma("unroll") for (int mt = 0; mt < FMT; ++mt)                                              \
+  _Pragma("unroll") for (int mt = 0; mt < NB; ++mt)                                               \
   _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                   \
       acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[mt].F, bb[j].F, acc[mt][j], 0, 0, 0);   \
-  accX = __builtin_amdgcn_mfma_f32_16x16x4f32(ax.F, bb[3].F, accX, 0, 0, 0);                      \
-  if (w == 0) accX2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[FMT - 1].F, bb[3].F, accX2, 0, 0, 0);
-        NRMS_KSTEP(x) NRMS_KSTEP(y) NRMS_KSTEP(z) NRMS_KSTEP(w)
+  if (w < NB) accX = __builtin_amdgcn_mfma_f32_16x16x4f32(ax.F, bb[3].F, accX, 0, 0, 0);           \
+  if (NB == 5 && w == 0) accX2 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[NB - 1].F, bb[3].F, accX2, 0, 0, 0);
+            NRMS_KSTEP(x) NRMS_KSTEP(y) NRMS_KSTEP(z) NRMS_KSTEP(w)
 #undef NRMS_KSTEP
-        if (c + 1 < FKG) {
+            if (c + 1 < FKG) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) bb[j] = bn[j];
+              for (int j = 0; j < 4; ++j) bb[j] = bn4[j];
+            }
+          }
+        }
+        NRMS_STAMP(3)
+        // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
+        // The next group's Q|K slices go out one token per M-tile, between the
+        // tanh blocks (pinned by sched_barrier): issued all at once ahead of the
+        // tanh work, the in-order issue stalls the VALU behind the gather's
+        // address/TA queue.
+#pragma unroll
+        for (int mt = 0; mt < NB; ++mt) {
+          if (mt < nb_next) prefetch_qk_tok(nbuf, mt);
+          else zero_qk_tok(mt);
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float p = 0.f;
+#pragma unroll
+            for (int j = 0; j < 3; ++j) p = fmaf(qv[j], tanh_fast(acc[mt][j][r] + bv[j]), p);
+            p = row16_sum(p);
+            const int row = 16 * mt + 4 * kq + r;
+            if (lm == 0) part[PART_STRIDE * row + w] = p;
+            const bool own_x = (mt == w && w < NB) || (NB == 5 && w == 0 && mt == 4);
+            if (own_x) {
+              const float ax = (NB == 5 && mt == 4) ? accX2[r] : accX[r];
+              float px = fmaf(qx, tanh_fast(ax + bx), 0.f);
+              px = row16_sum(px);
+              if (lm == 0) part[PART_STRIDE * row + 4] = px;
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#pragma unroll
+        for (int j = NB; j < 5; ++j) {
+          if (j < nb_next) prefetch_qk_tok(nbuf, j);
+          else zero_qk_tok(j);
         }
       }
-      }
-      NRMS_STAMP(3)
-      // C/D layout of 16x16 MFMA: col = lane & 15, row = (lane >> 4) * 4 + reg.
-      // The next group's Q|K slices go out one token per M-tile, between the
-      // tanh blocks (pinned by sched_barrier): issued all at once ahead of the
-      // tanh work, the in-order issue stalls the VALU behind the gather's
-      // address/TA queue (measured 3 % slower for the whole kernel).
-#pragma unroll
-      for (int mt = 0; mt < FMT; ++mt) {
-        prefetch_qk_tok(nbuf, mt);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float p = 0.f;
-#pragma unroll
-          for (int j = 0; j < 3; ++j) p = fmaf(qv[j], tanh_fast(acc[mt][j][r] + bv[j]), p);
-          if (xok && mt == w) p = fmaf(qx, tanh_fast(accX[r] + bx), p);
-          if (xok && w == 0 && mt == FMT - 1) p = fmaf(qx, tanh_fast(accX2[r] + bx), p);
-          p = row16_sum(p);
-          if (lm == 0) part[4 * (16 * mt + 4 * kq + r) + w] = p;   // [row][wave]
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    NRMS_STAMP(4)
-    __syncthreads();   // row partials complete
-    NRMS_STAMP(5)
+      NRMS_STAMP(4)
+      __syncthreads();   // row partials complete
+      NRMS_STAMP(5)
 
-    // ---------------- C: softmax over tokens + pooling from the O registers ----------------
-    // Lane (block (at, hl), x) holds rows 4i + x (i < 5) of title at, head h:
-    // the 4 lanes of a block see all 20 tokens, so the softmax (max-subtracted,
-    // as F.softmax) and the pooling out[20h + d] = sum_l w_l ctx[l][20h + d]
-    // reduce within the lane quad (DPP); the LDS tile is not read.
-    {
-      float sc[5];
+      // ---------------- C: softmax over tokens + pooling from the O registers ----------------
+      // Lane (block (at, hl), x) holds rows 4i + x (i < NB) of title at, head h:
+      // the 4 lanes of a block see all its rows, so the softmax (max-subtracted,
+      // as F.softmax) and the pooling out[20h + d] = sum_l w_l ctx[l][20h + d]
+      // reduce within the lane quad (DPP); the LDS tile is not read. Row 4i + x
+      // counts 1 (a real token), n_pad (the rep) or 0 (an unused slot).
+      {
+        float sc[NB], mult[NB];
 #pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        const float4 pv = *reinterpret_cast<const float4*>(part + 4 * (FL * at + 4 * i + x));
-        sc[i] = ((pv.x + pv.y) + pv.z) + pv.w;
-      }
-      if constexpr (H3) {
-        // a NaN score: an operand beyond fp16's range (or NaN inputs) -> recheck pass
-        bool bad = false;
-#pragma unroll
-        for (int i = 0; i < 5; ++i) bad |= sc[i] != sc[i];
-        recheck |= __builtin_amdgcn_ballot_w64(bad);
-      }
-      if constexpr (!EXACT) {
-        if (recheck != 0 && lane == 0) rl.list[atomicAdd(rl.count, 1)] = (int32_t)tg;
-      }
-      float mx = sc[0];
-#pragma unroll
-      for (int i = 1; i < 5; ++i) mx = nan_max(mx, sc[i]);
-      mx = nan_max(mx, quad_xor1(mx));
-      mx = nan_max(mx, quad_xor2(mx));
-      float ex[5], sum = 0.f;
-#pragma unroll
-      for (int i = 0; i < 5; ++i) {
-        ex[i] = expf(sc[i] - mx);
-        sum += ex[i];
-      }
-      sum += quad_xor1(sum);
-      sum += quad_xor2(sum);
-      float wt[5];
-#pragma unroll
-      for (int i = 0; i < 5; ++i) wt[i] = ex[i] / sum;
-      // pz[m][r'] = dim 5r' + m of head h, summed over this lane's 5 queries, then the quad
-      float pz[5][4];
-#pragma unroll
-      for (int m = 0; m < 5; ++m)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float a = 0.f;
-#pragma unroll
-          for (int i = 0; i < 5; ++i) a = fmaf(wt[i], O[m][i][r], a);
-          a += quad_xor1(a);
-          pz[m][r] = a + quad_xor2(a);
+        for (int i = 0; i < NB; ++i) {
+          const int row = LR * at + 4 * i + x;
+          const float4 pv = *reinterpret_cast<const float4*>(part + PART_STRIDE * row);
+          sc[i] = (((pv.x + pv.y) + pv.z) + pv.w) + part[PART_STRIDE * row + 4];
+          const int q = 4 * i + x;
+          mult[i] = q < my_c ? 1.f : ((q == my_c && npad > 0) ? (float)npad : 0.f);
         }
-      const int64_t s = tg * FT + at;
-      if (hval && s < rmap.n_titles) {
-        // lane x stores dims 5x .. 5x + 4 of head h
-        float v[5];
+        if constexpr (H3) {
+          // a NaN score: an operand beyond fp16's range (or NaN inputs) -> recheck pass
+          bool bad = false;
+#pragma unroll
+          for (int i = 0; i < NB; ++i) bad |= mult[i] > 0.f && sc[i] != sc[i];
+          recheck |= __builtin_amdgcn_ballot_w64(bad);
+        }
+        if constexpr (!EXACT) {
+          // titles of the flagged lanes (title at = lanes 16 at .. 16 at + 15)
+          int tm = 0;
+#pragma unroll
+          for (int t = 0; t < FT; ++t) tm |= ((recheck >> (16 * t)) & 0xFFFFull) ? (1 << t) : 0;
+          if (tm != 0 && lane == 0) rl.list[atomicAdd(rl.count, 1)] = (int32_t)((k << 4) | tm);
+        }
+        float mx = -INFINITY;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) mx = mult[i] > 0.f ? nan_max(mx, sc[i]) : mx;
+        mx = nan_max(mx, quad_xor1(mx));
+        mx = nan_max(mx, quad_xor2(mx));
+        float ex[NB], sum = 0.f;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          ex[i] = mult[i] > 0.f ? expf(sc[i] - mx) * mult[i] : 0.f;
+          sum += ex[i];
+        }
+        sum += quad_xor1(sum);
+        sum += quad_xor2(sum);
+        float wt[NB];
+#pragma unroll
+        for (int i = 0; i < NB; ++i) wt[i] = ex[i] / sum;
+        // pz[m][r'] = dim 5r' + m of head h, summed over this lane's rows, then
+        // the quad; unused slots (last row block only) are skipped, not
+        // weighted by 0 (their context may be non-finite)
+        float pz[5][4];
 #pragma unroll
         for (int m = 0; m < 5; ++m)
-          v[m] = x == 0 ? pz[m][0] : (x == 1 ? pz[m][1] : (x == 2 ? pz[m][2] : pz[m][3]));
-        float* dst = out + s * FD + FDK * h + 5 * x;
-        float4_a4 v4;
-        v4.x = v[0]; v4.y = v[1]; v4.z = v[2]; v4.w = v[3];
-        *reinterpret_cast<float4_a4*>(dst) = v4;
-        dst[4] = v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float a = 0.f;
+#pragma unroll
+            for (int i = 0; i < NB; ++i)
+              a = (i < NB - 1 || mult[i] > 0.f) ? fmaf(wt[i], O[m][i][r], a) : a;
+            a += quad_xor1(a);
+            pz[m][r] = a + quad_xor2(a);
+          }
+        const int32_t my_s = tmeta[8 * buf + at];   // this lane's title (-1: none)
+        const bool write = hval && my_s >= 0 && (!EXACT || ((tmask >> at) & 1));
+        if (write) {
+          // lane x stores dims 5x .. 5x + 4 of head h
+          float v[5];
+#pragma unroll
+          for (int m = 0; m < 5; ++m)
+            v[m] = x == 0 ? pz[m][0] : (x == 1 ? pz[m][1] : (x == 2 ? pz[m][2] : pz[m][3]));
+          float* dst = out + (int64_t)my_s * FD + FDK * h + 5 * x;
+          float4_a4 v4;
+          v4.x = v[0]; v4.y = v[1]; v4.z = v[2]; v4.w = v[3];
+          *reinterpret_cast<float4_a4*>(dst) = v4;
+          dst[4] = v[4];
+        }
+        // V slices of the next group: issued here, after O is dead (holding both
+        // through the B epilogue spills); the S^T phase of the next group covers
+        // most of their latency
+        prefetch_v(nbuf, nb_next);
       }
-      // V slices of the next group: issued here, after O is dead (holding both
-      // through the B epilogue spills); the S^T phase of the next group covers
-      // most of their latency (measured wait ~1.3k cycles per group)
-      prefetch_v(nbuf);
+      NRMS_STAMP(6)
     }
-    NRMS_STAMP(6)
+    ++it;
+  };
+  if constexpr (EXACT) {
+    // flagged groups in list order, any bucket
+    for (int64_t idx = blockIdx.x; idx < n_iter; idx += gridDim.x) {
+      int tm;
+      int64_t g;
+      switch (bucket_of(key_at(idx, tm), g)) {
+        case 0: iterate(idx, std::integral_constant<int, 1>{}); break;
+        case 1: iterate(idx, std::integral_constant<int, 2>{}); break;
+        case 2: iterate(idx, std::integral_constant<int, 3>{}); break;
+        case 3: iterate(idx, std::integral_constant<int, 4>{}); break;
+        default: iterate(idx, std::integral_constant<int, 5>{}); break;
+      }
+    }
+  } else {
+    // the main pass walks the buckets' contiguous group ranges one after the
+    // other, one loop per NB (a single loop switching between the five bodies
+    // spilled ~600 registers)
+    auto run_bucket = [&](auto nbc) {
+      constexpr int NB = decltype(nbc)::value;
+      const int64_t start = NB == NBK ? 0 : __builtin_amdgcn_readfirstlane(sched[NB]);
+      const int64_t end = __builtin_amdgcn_readfirstlane(sched[NB - 1]);
+      const int64_t grid = gridDim.x;
+      int64_t idx = start + (((int64_t)blockIdx.x - start) % grid + grid) % grid;
+      for (; idx < end; idx += grid) iterate(idx, nbc);
+    };
+    run_bucket(std::integral_constant<int, 5>{});
+    run_bucket(std::integral_constant<int, 4>{});
+    run_bucket(std::integral_constant<int, 3>{});
+    run_bucket(std::integral_constant<int, 2>{});
+    run_bucket(std::integral_constant<int, 1>{});
   }
 #ifdef NRMS_FUSED_TIMING
   if (!EXACT && lane == 0)
@@ -958,26 +1193,49 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 
 }  // namespace
 
-// packed W_add + special rows, then int32 [recheck count, group-list count,
-// rep, user row-list count] (zeroed / rep = INT32_MAX by the pack kernel of
-// every launch), the recheck list (4 per group), the group list, pad_group
-// bytes
+// Workspace after the packed W_add, special rows and f16 planes: int32
+// counters [NCNT] (reset by the pack kernel of every launch), the recheck list
+// (4 per group), the bucket lists [NBK][n], the compacted rows [n][20], then
+// bytes: counts [n] and all-padding flags [n].
 static size_t fused_news_list_offset() { return (size_t)WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS; }
+static int64_t max_groups(int64_t n_titles) { return (n_titles + FT - 1) / FT + NBK; }
 size_t fused_news_workspace_floats(int64_t n_titles) {
-  const int64_t n_groups = (n_titles + FT - 1) / FT;
-  return fused_news_list_offset() + 4 + 4 * (size_t)n_groups + (size_t)n_groups +
-         ((size_t)n_groups + 3) / 4;
+  return fused_news_list_offset() + NCNT + 4 * (size_t)max_groups(n_titles) + (size_t)NBK * n_titles +
+         (size_t)FL * n_titles + ((size_t)2 * n_titles + 3) / 4;
 }
+namespace {
+struct NewsWs {
+  int32_t* counters;
+  int32_t* recheck;
+  int32_t* list;
+  int32_t* crow;
+  uint8_t* cnt;
+  uint8_t* pad_title;
+};
+NewsWs news_ws(float* ws, int64_t n_titles) {
+  NewsWs z;
+  z.counters = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
+  z.recheck = z.counters + NCNT;
+  z.list = z.recheck + 4 * max_groups(n_titles);
+  z.crow = z.list + NBK * n_titles;
+  z.cnt = reinterpret_cast<uint8_t*>(z.crow + FL * n_titles);
+  z.pad_title = z.cnt + n_titles;
+  return z;
+}
+}  // namespace
 
 static std::atomic<int> g_title_dedupe{[] {
   const char* e = getenv("NRMS_DEDUPE");
   return (e && e[0] == '0') ? 0 : 1;
 }()};
+static std::atomic<int> g_token_compaction{[] {
+  const char* e = getenv("NRMS_COMPACT");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
 int title_dedupe() { return g_title_dedupe.load(std::memory_order_relaxed); }
-static bool dedupe_applies(int dedupe, const int64_t* ids_a, const int64_t* ids_b) {
-  return dedupe && ids_a != nullptr && (((uintptr_t)ids_a | (uintptr_t)(ids_b ? ids_b : ids_a)) % 16) == 0;
-}
 int set_title_dedupe(int on) { return g_title_dedupe.exchange(on ? 1 : 0); }
+int token_compaction() { return g_token_compaction.load(std::memory_order_relaxed); }
+int set_token_compaction(int on) { return g_token_compaction.exchange(on ? 1 : 0); }
 
 bool fused_news_supported(int L, int D, int H, int Q) {
   return L == FL && D == FD && H == FH && Q == FQ;
@@ -994,13 +1252,13 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting, bool* deduped,
-                          int64_t broadcast_from, int64_t* user_list, int64_t user_rows, bool prepacked) {
+                          int64_t broadcast_from, int64_t* user_list, int64_t user_rows, bool prepacked,
+                          bool direct_rows, int compact_setting) {
   if (deduped) *deduped = false;
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
   if (ldq < ROW || ldq % 4) return NRMS_ERR_UNSUPPORTED;   // float4 q / k slices
-  const int64_t n_groups = (n_titles + FT - 1) / FT;
-  if (4 * n_groups > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  if (max_groups(n_titles) >= (1ll << 27)) return NRMS_ERR_UNSUPPORTED;   // recheck entries: group << 4 | mask
   // F16X3: f16x3 main pass, x6 recheck pass
   const int arith = gemm_arith();
   const bool h3 = arith == NRMS_GEMM_SPLIT_F16X3;
@@ -1011,30 +1269,37 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   const size_t lds_bytes_exact = x6 ? LDS_BYTES_X6 : LDS_BYTES;
   ensure_dynamic_lds(reinterpret_cast<const void*>(kern), (int)lds_bytes);
   ensure_dynamic_lds(reinterpret_cast<const void*>(kern_exact), (int)lds_bytes_exact);
-  int32_t* rcount = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
-  const RecheckList rl{rcount, rcount + 4};
-  int32_t* glist = rcount + 4 + 4 * n_groups;
-  uint8_t* pad_group = reinterpret_cast<uint8_t*>(glist + n_groups);
-  // padding-group dedupe needs the token ids (gathered rows), 16-B aligned id rows
-  const bool dedupe = dedupe_applies(dedupe_setting < 0 ? title_dedupe() : dedupe_setting, ids_a, ids_b);
-  const GroupList gl{dedupe ? glist : nullptr, rcount + 1, rcount + 2};
+  const NewsWs z = news_ws(ws, n_titles);
+  const RecheckList rl{z.counters + CNT_RECHECK, z.recheck};
+  // classification (title dedupe and / or token compaction) needs the token
+  // ids as 16-B aligned rows, and row ids / title indices that fit int32
+  const int dedupe_on = dedupe_setting < 0 ? title_dedupe() : dedupe_setting;
+  const int compact_on = compact_setting < 0 ? token_compaction() : compact_setting;
+  const int64_t row_span = direct_rows ? n_titles * FL : n_rows;
+  const bool classify = ids_a != nullptr && (dedupe_on || compact_on) &&
+                        (((uintptr_t)ids_a | (uintptr_t)(ids_b ? ids_b : ids_a)) % 16) == 0 &&
+                        row_span <= INT32_MAX && n_titles <= INT32_MAX;
+  const bool dedupe = classify && dedupe_on;
+  const bool compact = classify && compact_on;
+  const TitleSet ts{classify ? z.crow : nullptr, z.cnt, classify ? z.list : nullptr, z.counters, n_titles,
+                    compact ? 0 : NBK - 1};
   // the UserEncoder's row list (nrms_forward) in the main pass's prologue
-  const UserRows ur{dedupe && user_list && user_rows > 0 ? user_list : nullptr, user_rows, pad_group, rcount + 2,
-                    rcount + 3};
+  const UserRows ur{dedupe && user_list && user_rows > 0 ? user_list : nullptr, user_rows, z.pad_title,
+                    z.counters + CNT_REP, z.counters + CNT_USER};
   if (prepacked) {
     // (forward_pack_kernel packed W_add and reset the counters)
   } else if (x6) {
     const int npk = XKS * FNT * 64 * 8 + SPECIAL_FLOATS;
     if (h3)
       hipLaunchKernelGGL(pack_additive_b3_kernel<true>, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
-                         rcount);
+                         z.counters);
     else
       hipLaunchKernelGGL(pack_additive_b3_kernel<false>, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
-                         rcount);
+                         z.counters);
   } else {
     const int npk = WAP_FLOATS + SPECIAL_FLOATS;
     hipLaunchKernelGGL(pack_additive_b_kernel, dim3((npk + 255) / 256), dim3(256), 0, s, w_add, ws,
-                       rcount);
+                       z.counters);
   }
   if (int32_t st = launch_status()) return st;
   int dev = 0, n_cu = 256;
@@ -1043,28 +1308,30 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
       n_cu = v;
   }
-  const int64_t blocks = n_groups < n_cu ? n_groups : n_cu;   // persistent: one workgroup per CU
-  RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows};
-  if (dedupe) {
-    hipLaunchKernelGGL(classify_groups_kernel, dim3((unsigned)((4 * n_groups + CLS_T - 1) / CLS_T)), dim3(CLS_T),
-                       0, s, rm, n_groups, glist, rcount + 1, rcount + 2, pad_group);
+  const int64_t groups = classify ? max_groups(n_titles) : (n_titles + FT - 1) / FT;
+  const int64_t blocks = groups < n_cu ? groups : n_cu;   // persistent: one workgroup per CU
+  const RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows, direct_rows};
+  if (classify) {
+    const Titles tt{z.crow, z.cnt, z.pad_title, z.list, z.counters, n_titles};
+    hipLaunchKernelGGL(classify_titles_kernel, dim3((unsigned)((n_titles + CLS_T - 1) / CLS_T)), dim3(CLS_T), 0, s,
+                       rm, tt, dedupe ? 1 : 0, compact ? 1 : 0);
     if (int32_t st = launch_status()) return st;
   }
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, gl, ws,
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NTHR), lds_bytes, s, qkv, ldq, rm, ts, ws,
                      b_add, q_add, out, rl, ur NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
   // the recheck pass: reads the count the main pass left; exits at once when 0
   const int64_t blocks_x = blocks < 64 ? blocks : 64;
-  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes_exact, s, qkv, ldq, rm, gl,
+  hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes_exact, s, qkv, ldq, rm, ts,
                      ws, b_add, q_add, out, rl, UserRows{nullptr, 0, nullptr, nullptr, nullptr} NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
   // (titles below broadcast_from are not copied: nrms_forward's UserEncoder
-  // reads the clicked padding titles from the rep group's rows)
-  const int64_t b0 = broadcast_from < 0 ? 0 : (broadcast_from / FT) * FT;
+  // reads the clicked padding titles from the rep title's rows)
+  const int64_t b0 = broadcast_from < 0 ? 0 : broadcast_from;
   if (dedupe && b0 < n_titles) {
     const int64_t nt4 = (n_titles - b0) * (FD / 4);
     hipLaunchKernelGGL(broadcast_padding_kernel, dim3((unsigned)((nt4 + 255) / 256)), dim3(256), 0, s,
-                       pad_group, rcount + 2, b0, n_titles, out);
+                       z.pad_title, z.counters + CNT_REP, b0, n_titles, out);
   }
   const int32_t st = launch_status();
   if (st == NRMS_OK && deduped) *deduped = dedupe;
@@ -1072,17 +1339,14 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
 }
 
 PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles) {
-  const int64_t n_groups = (n_titles + FT - 1) / FT;
-  int32_t* rcount = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
-  int32_t* glist = rcount + 4 + 4 * n_groups;
-  return PaddingGroups{reinterpret_cast<const uint8_t*>(glist + n_groups), rcount + 2, rcount + 3};
+  const NewsWs z = news_ws(ws, n_titles);
+  return PaddingGroups{z.pad_title, z.counters + CNT_REP, z.counters + CNT_USER};
 }
 
 int32_t launch_user_row_list(const PaddingGroups& pg, int64_t n_rows, int64_t* list, hipStream_t s) {
   if (n_rows == 0) return NRMS_OK;
-  int32_t* count = pg.user_count;
   hipLaunchKernelGGL(user_row_list_kernel, dim3((unsigned)((n_rows + URL_ROWS - 1) / URL_ROWS)), dim3(256), 0, s,
-                     pg.pad_group, pg.rep, n_rows, list, count);
+                     pg.pad_title, pg.rep, n_rows, list, pg.user_count);
   return launch_status();
 }
 

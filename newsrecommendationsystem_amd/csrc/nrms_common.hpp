@@ -233,18 +233,19 @@ int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, flo
                     float b2, float eps, int64_t step, hipStream_t s);
 
 // Device-side padding classification a deduplicating fused-news launch left
-// in its workspace: pad_group[g] = 1 for all-padding 4-title groups, and title
-// 4g + t of such a group (g != *rep) carries a copy of title 4 rep + t.
+// in its workspace: pad_title[t] = 1 for all-padding titles (20 zero ids), and
+// every such title t != *rep carries a copy of title *rep's vector (computed
+// once; the computation of a title does not depend on where it is encoded).
 // user_count: the launch's (zeroed) slot for launch_user_row_list's count.
 struct PaddingGroups {
-  const uint8_t* pad_group;
+  const uint8_t* pad_title;
   const int32_t* rep;
   int32_t* user_count;
 };
 size_t fused_user_packed_b_floats();
 bool fused_user_supported(int L, int D, int H, int Q);
 // pg (optional): rows m = b L + i of copied padding titles (see
-// PaddingGroups) are read from 4 rep + m % 4.
+// PaddingGroups) are read from row *rep.
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
                           hipStream_t s, const PaddingGroups* pg = nullptr, bool prepacked = false);
@@ -253,25 +254,33 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
 // environment turns it off).
 int title_dedupe();
 int set_title_dedupe(int on);
+// Process-wide switch (news_fused.hip): token compaction -- the id-0 tokens of
+// a title share one q|k|v row, so the news tail encodes each distinct padding
+// row once with its multiplicity (nrms_set_token_compaction; NRMS_COMPACT=0
+// turns it off).
+int token_compaction();
+int set_token_compaction(int on);
 
 // workspace of launch_fused_news: packed W_add, special rows, recheck list
 size_t fused_news_workspace_floats(int64_t n_titles);
 bool fused_news_supported(int L, int D, int H, int Q);
-// dedupe_setting: -1 = the process-wide nrms_set_title_dedupe setting, else
-// 0 / 1; *deduped (optional) tells whether the padding groups were classified
+// dedupe_setting / compact_setting: -1 = the process-wide setting
+// (nrms_set_title_dedupe / nrms_set_token_compaction), else 0 / 1; *deduped
+// (optional) tells whether the padding titles were classified
 // (fused_news_padding_groups is then valid until the workspace is reused).
-// broadcast_from: the copies of the rep group's vectors are written for titles
-// >= broadcast_from (rounded down to a group) only. user_list (optional): when
-// the launch deduplicates, the main pass also builds launch_user_row_list's
-// list of titles 0 .. user_rows - 1 (count in the PaddingGroups user_count).
-// prepacked: ws already holds the packed W_add and reset counters
-// (launch_forward_pack).
+// broadcast_from: the copies of the rep title's vector are written for titles
+// >= broadcast_from only. user_list (optional): when the launch deduplicates,
+// the main pass also builds launch_user_row_list's list of titles
+// 0 .. user_rows - 1 (count in the PaddingGroups user_count). prepacked: ws
+// already holds the packed W_add and reset counters (launch_forward_pack).
+// direct_rows: the q|k|v rows are per token (row s L + i, the per-token
+// projection); the ids (if any) only classify the tokens.
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr,
                           int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0,
-                          bool prepacked = false);
+                          bool prepacked = false, bool direct_rows = false, int compact_setting = -1);
 PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles);
 // The rows m < n_rows of titles not copied from rep (the UserEncoder's rows to
 // project), appended to list in any order; their count in *pg.user_count.
@@ -282,8 +291,8 @@ int32_t launch_score_pairs(const float* news, int64_t n_news, const float* user,
 int32_t launch_impression_metrics(const float* scores, const int32_t* labels,
                                   const int64_t* offsets, int64_t n_imp, double* out,
                                   hipStream_t s);
-// pg (optional): candidates of copied all-padding groups read the rep group's
-// vector; the candidates are titles title0 + b C + c of a contiguous array
+// pg (optional): candidates that are copied all-padding titles read the rep
+// title's vector; the candidates are titles title0 + b C + c of a contiguous array
 // (news points at title0's row).
 int32_t launch_score(const float* news, int64_t B, int C, int64_t sb, int64_t sc,
                      const float* user, int64_t su, int D, float* out, hipStream_t s,

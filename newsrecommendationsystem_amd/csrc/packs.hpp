@@ -20,7 +20,10 @@ constexpr int NEWS_WAP_F32 = KG * NT * 64 * 4;
 constexpr int NEWS_WAP_X6 = KS * NT * 3 * 64 * 4;
 constexpr int NEWS_WAP_MAX = NEWS_WAP_X6 > NEWS_WAP_F32 ? NEWS_WAP_X6 : NEWS_WAP_F32;
 constexpr int NEWS_SPECIAL = 2 * ROW;
-constexpr int NEWS_COUNTERS = NEWS_WAP_MAX + NEWS_SPECIAL + NEWS_WAP_X6;   // int32 [4] after the f16 planes
+constexpr int NEWS_COUNTERS = NEWS_WAP_MAX + NEWS_SPECIAL + NEWS_WAP_X6;   // int32 [NEWS_NCOUNT] after the f16 planes
+// the news launch's counters: [recheck count, title-bucket counts 0..4, rep
+// title (INT32_MAX: none), user row-list count]
+constexpr int NEWS_NCOUNT = 8, NEWS_CNT_REP = 6;
 constexpr int NEWS_X6_ELEMS = KS * NT * 64 * 8;   // threads of the x6 / f16 packing
 constexpr int USER_X6_ELEMS = KS * NT * 64 * 8;
 constexpr int USER_F32_ELEMS = KG * NT * 64 * 4;
@@ -37,11 +40,11 @@ __device__ __forceinline__ void split3(float x, __bf16& hi, __bf16& mid, __bf16&
 // x6 planes [ks][nt][plane][lane][8] (bf16 hi | mid | lo of Wa[16 nt + (lane
 // & 15)][32 ks + 8 (lane >> 4) + i], 0 past Q or D); F16: also the fp16 planes
 // (2^11 hi, 2^11-scaled residual, hi) after the special rows; then the zero
-// and NaN q|k|v rows; idx < 4 resets the launch's counters.
+// and NaN q|k|v rows; idx < NEWS_NCOUNT resets the launch's counters.
 template <bool F16>
 __device__ __forceinline__ void pack_news_additive(int idx, const float* __restrict__ Wa, float* __restrict__ WaP,
                                                    int32_t* __restrict__ counters) {
-  if (idx < 4) counters[idx] = idx == 2 ? INT32_MAX : 0;
+  if (idx < NEWS_NCOUNT) counters[idx] = idx == NEWS_CNT_REP ? INT32_MAX : 0;
   if (idx >= NEWS_X6_ELEMS + NEWS_SPECIAL) return;
   if (idx >= NEWS_X6_ELEMS) {
     const int sidx = idx - NEWS_X6_ELEMS;

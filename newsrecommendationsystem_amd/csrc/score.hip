@@ -10,8 +10,8 @@ constexpr int kScoreThreads = 256;
 
 // pg (optional, nrms_forward after padding-title dedupe): the candidates are
 // titles title0 + b C + c of a contiguous [titles, D] array (news = its row
-// title0); a candidate in a copied all-padding group reads the rep group's
-// vector instead (PaddingGroups), so no copies need to be written.
+// title0); a copied all-padding candidate reads the rep title's vector
+// instead (PaddingGroups), so no copies need to be written.
 __global__ __launch_bounds__(kScoreThreads) void score_kernel(
     const float* __restrict__ news, int64_t B, int C, int64_t sb, int64_t sc,
     const float* __restrict__ user, int64_t su, int D, float* __restrict__ out, PaddingGroups pg,
@@ -22,9 +22,9 @@ __global__ __launch_bounds__(kScoreThreads) void score_kernel(
   const int64_t b = pair / C;
   const int c = (int)(pair - b * C);
   const float* nv = news + b * sb + (int64_t)c * sc;
-  if (pg.pad_group) {
-    const int64_t t = title0 + pair, g = t >> 2, r = *pg.rep;
-    if (pg.pad_group[g] && g != r) nv = news + (4 * r + (t & 3) - title0) * D;
+  if (pg.pad_title) {
+    const int64_t t = title0 + pair, r = *pg.rep;
+    if (pg.pad_title[t] && t != r) nv = news + (r - title0) * D;
   }
   const float* uv = user + b * su;
   float acc = 0.f;

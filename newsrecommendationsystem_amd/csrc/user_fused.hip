@@ -121,10 +121,10 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // q|k|v row of position i (stride ldq floats); with pg, a position holding a
   // copied padding title reads the row of the title it copies
-  const int32_t rep = pg.pad_group ? *pg.rep : 0;
+  const int32_t rep = pg.pad_title ? *pg.rep : 0;
   auto row = [&](int i) -> const float* {
     int64_t m = s * L + i;
-    if (pg.pad_group && pg.pad_group[m >> 2] && (m >> 2) != rep) m = 4 * (int64_t)rep + (m & 3);
+    if (pg.pad_title && pg.pad_title[m] && m != rep) m = rep;
     return qkv + m * ldq;
   };
 

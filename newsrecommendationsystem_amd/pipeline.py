@@ -132,17 +132,20 @@ class ForwardPlan:
 
     # Algorithmic work per launch of each stage (SURVEY §8d conventions:
     # GEMMs 2·M·N·K; bytes = operands the stage must read + results it writes).
-    def work(self, titles_encoded=None, user_rows_projected=None):
+    def work(self, titles_encoded=None, user_rows_projected=None, news_rows=None):
         """titles_encoded: titles the fused news tail actually encodes (with
-        padding-title dedupe: the titles of the non-padding 4-title groups + one
-        padding group); user_rows_projected: clicked rows the UserEncoder's
-        Q|K|V GEMM projects (with dedupe: all but the copied padding rows);
-        default all."""
+        padding-title dedupe: the titles with a real token + one all-padding
+        title); user_rows_projected: clicked rows the UserEncoder's Q|K|V GEMM
+        projects (with dedupe: all but the copied padding rows); news_rows:
+        (sum of Le, sum of Le^2) over the encoded titles, Le = the distinct q|k|v
+        rows a title is encoded on (token compaction: real tokens + one padding
+        row; L without it); default all titles, L rows each."""
         B, C, Nc, L, D, V = self.B, self.C, self.N, self.L, self.D, self.V
         Q, H, dk = 200, 15, D // 15
         n_all, n_clk = B * (C + Nc), B * Nc
         n_enc = n_all if titles_encoded is None else titles_encoded
         n_up = n_clk if user_rows_projected is None else user_rows_projected
+        rows, rows_sq = (n_enc * L, n_enc * L * L) if news_rows is None else news_rows
         att_flop = lambda seqs, l: seqs * H * 2 * (2 * l * l * dk)
         qkv_m = V if self.folded else n_all * L
         return {
@@ -155,11 +158,13 @@ class ForwardPlan:
             "pool_news": dict(flop=2 * n_all * L * D, bytes=4 * (n_all * L * (D + 1) + n_all * D)),
             # fused tail: gathered q|k|v rows + ids in, news vectors out, W_add
             # (the context tile stays in LDS)
-            "news_fused": dict(flop=att_flop(n_enc, L) + 2 * n_enc * L * D * Q + 2 * n_enc * L * D,
-                               bytes=n_enc * L * (4 * 3 * D + (8 if self.folded else 0))
+            # (per title on Le rows: attention 2 contractions x H heads x 2 Le^2 dk,
+            # additive GEMM 2 Le D Q, pooling 2 Le D)
+            "news_fused": dict(flop=H * 4 * rows_sq * dk + 2 * rows * D * Q + 2 * rows * D,
+                               bytes=rows * 4 * 3 * D + n_enc * L * (8 if self.folded else 0)
                                + 4 * (n_all * D + Q * D),
-                               split=dict(attention=att_flop(n_enc, L), gemm=2 * n_enc * L * D * Q,
-                                          pool=2 * n_enc * L * D)),
+                               split=dict(attention=H * 4 * rows_sq * dk, gemm=2 * rows * D * Q,
+                                          pool=2 * rows * D)),
             "qkv_user": dict(flop=2 * n_up * D * 3 * D, bytes=4 * (n_up * 4 * D + 3 * D * D)),
             "mhsa_user": dict(flop=att_flop(B, Nc), bytes=4 * n_clk * 4 * D),
             "addscore_user": dict(flop=2 * n_clk * D * Q, bytes=4 * (n_clk * (D + 1) + Q * D)),

@@ -46,9 +46,12 @@ int main(int argc, char** argv) {
   for (auto& v : h_wa) v = (rnd() - 0.5f) * 0.1f;
   for (auto& v : h_b) v = (rnd() - 0.5f) * 0.1f;
   for (auto& v : h_q) v = (rnd() - 0.5f) * 0.2f;
-  for (size_t i = 0; i < h_ids.size(); ++i) h_ids[i] = 1 + (int64_t)(rnd() * id_range);
-  // a few padding tokens / an all-padding title, as the synthetic generator has
-  for (int t = 0; t < 20; ++t) h_ids[7 * 20 + t] = 0;
+  // titles of the bench's stream: length U{5..20}, right-padded with id 0
+  for (int64_t s = 0; s < n_titles; ++s) {
+    const int len = 5 + (int)(rnd() * 16);
+    for (int t = 0; t < 20; ++t) h_ids[s * 20 + t] = t < len ? 1 + (int64_t)(rnd() * id_range) : 0;
+  }
+  for (int t = 0; t < 20; ++t) h_ids[7 * 20 + t] = 0;   // an all-padding title
   float *qkv, *wa, *b, *q, *wap, *out0, *out1, *out2;
   int64_t* ids;
   unsigned long long* dbg;
@@ -77,7 +80,12 @@ int main(int argc, char** argv) {
   const int nwaves[3] = {4, 4, 4};
   const int arith[3] = {NRMS_GEMM_F32, NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_SPLIT_F16X3};
   float* outs[3] = {out0, out1, out2};
+  const int compact_runs = getenv("NV_BOTH") ? 2 : 1;
+  for (int cr = 0; cr < compact_runs; ++cr)
   for (int var = 2; var >= 0; --var) {
+    if (getenv("NV_ONLY_H3") && var != 2) continue;
+    nrms::set_token_compaction(cr == 0 ? 1 : 0);
+    printf("token compaction %s\n", cr == 0 ? "on" : "off");
     nrms::g_arith = arith[var];
     float* out = outs[var];
     for (int it = 0; it < 2; ++it)

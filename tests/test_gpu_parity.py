@@ -392,7 +392,17 @@ def _stage_abi_matches_module(golden, golden_state, device):
     ws = torch.empty(nb, dtype=torch.uint8, device=device)
     N.call("nrms_news_attention_pool", N.ptr(qkv), 0, n * L, None, n, None, n, L, ctypes.byref(w),
            N.ptr(fused), N.ptr(ws), nb, st)
-    assert torch.equal(fused, ref)
+    # (no ids given: every token its own row) bitwise the module's path with
+    # token compaction off, and to fp32 rounding with it on
+    lib = N.load()
+    prev = lib.nrms_set_token_compaction(0)
+    try:
+        with torch.no_grad():
+            ref0 = m.get_news_vector({"title": ids.cpu()})
+    finally:
+        lib.nrms_set_token_compaction(prev)
+    assert torch.equal(fused, ref0)
+    assert (fused - ref).norm() / ref.norm() < 2e-6
     assert O.normwise_rel_err(_np(fused), golden["news_out"]).max() < TOL
     # stage 1 alone against the oracle's projection
     x = golden_state["news_encoder.word_embedding.weight"][golden["news_ids"].astype(np.int64)]
@@ -507,9 +517,11 @@ def test_plan_matches_forward(device, fused, mode, gemm_mode):
     with torch.no_grad():
         y = plan.run(c, k).clone()
         ref = m.forward_ids(c, k, proj_mode=mode)
-    if fused:
+    if fused and mode == 2:
         assert torch.equal(y, ref)
     else:
+        # (direct: the stage call gets per-token rows and no ids, so it runs
+        # without token compaction; nrms_forward compacts -- fp32 rounding)
         assert ((y - ref).norm() / ref.norm()) < 1e-5
     assert np.abs(_np(y) - O.forward(cand, clk, sd, np.float64)).max() <= TOL * np.abs(_np(y)).max()
 
@@ -778,6 +790,81 @@ def test_padding_title_dedupe_is_bitwise_identical(device, pad_frac, gemm_mode):
     if pad.any():   # one vector per slot; slots agree to fp32 rounding
         vp = outs[1][1][pad.to(device)]
         assert float((vp - vp[:1]).abs().max()) <= 1e-6 * float(vp.abs().max())
+
+
+def _set_switch(lib, name, on):
+    return getattr(lib, name)(on)
+
+
+@pytest.mark.parametrize("mode", ["folded", "direct"])
+def test_token_compaction_every_title_length(device, mode, gemm_mode):
+    """nrms_set_token_compaction: titles with 0..20 real tokens (right-padded,
+    plus interior zeros and a title of only interior padding) encoded with the
+    padding rows compacted agree with the uncompacted encoding to fp32
+    rounding, and both with the fp64 oracle (news_encoder.py:27-48)."""
+    from newsrecommendationsystem_amd import _native as N
+    V = 1500
+    sd = W.nrms_state(71, V)
+    pm = N.NRMS_PROJ_FOLDED if mode == "folded" else N.NRMS_PROJ_DIRECT
+    m = _module(sd, V, device, hip_proj_mode=pm, hip_cache_folded_table=False)
+    rng = np.random.default_rng(71)
+    rows = []
+    for rep in range(6):
+        for c in range(21):
+            t = np.zeros(20, np.int64)
+            t[:c] = rng.integers(1, V, c)
+            rows.append(t)
+    t = rng.integers(1, V, 20)
+    t[[2, 5, 6, 11, 19]] = 0          # interior zeros
+    rows.append(t)
+    t = np.zeros(20, np.int64)
+    t[[0, 7, 13]] = rng.integers(1, V, 3)
+    rows.append(t)
+    ids = np.stack(rows)
+    lib = N.load()
+    outs = {}
+    prev = lib.nrms_set_token_compaction(1)
+    try:
+        for on in (1, 0):
+            lib.nrms_set_token_compaction(on)
+            with torch.no_grad():
+                outs[on] = _np(m.get_news_vector({"title": torch.from_numpy(ids)}))
+    finally:
+        lib.nrms_set_token_compaction(prev)
+    assert np.isfinite(outs[1]).all()
+    assert O.normwise_rel_err(outs[1], outs[0]).max() < 2e-6
+    ref = O.news_encode(ids, sd, np.float64)
+    assert O.normwise_rel_err(outs[1], ref).max() < TOL
+    assert O.normwise_rel_err(outs[0], ref).max() < TOL
+    # a title's vector does not depend on where in the launch it is encoded
+    with torch.no_grad():
+        perm = rng.permutation(len(ids))
+        again = _np(m.get_news_vector({"title": torch.from_numpy(ids[perm])}))
+    assert np.array_equal(again, outs[1][perm])
+
+
+def test_token_compaction_forward_vs_oracle(device, gemm_mode):
+    """The config-3-shaped forward (left-padded histories, right-padded
+    titles) with and without token compaction, against the fp64 oracle."""
+    from newsrecommendationsystem_amd import _native as N
+    V, B = 4000, 48
+    sd = W.nrms_state(73, V)
+    m = _module(sd, V, device, hip_proj_mode=N.NRMS_PROJ_FOLDED)
+    cand, clk, _ = W.impressions(73, 9, B, V)
+    lib = N.load()
+    ys = {}
+    prev = lib.nrms_set_token_compaction(1)
+    try:
+        for on in (1, 0):
+            lib.nrms_set_token_compaction(on)
+            with torch.no_grad():
+                ys[on] = _np(m.forward_ids(torch.from_numpy(cand), torch.from_numpy(clk)))
+    finally:
+        lib.nrms_set_token_compaction(prev)
+    ref = O.forward(cand, clk, sd, np.float64)
+    scale = max(np.abs(ref).max(), 1e-6)
+    assert np.abs(ys[1] - ref).max() <= TOL * scale
+    assert np.abs(ys[1] - ys[0]).max() <= 1e-5 * scale
 
 
 def test_padding_title_dedupe_odd_batch_bitwise(device, gemm_mode):
