@@ -129,7 +129,7 @@ def cpu_baseline(model, cand, clk, reps=3):
                       f"({', '.join(f'{t:.2f}' for t in times)} s)"}
     parity = {"sample_impressions": B, "max_normwise_rel_err_logits": err,
               "tolerance": 1e-3, "ok": bool(err <= 1e-3)}
-    return info, parity
+    return info, parity, ref
 
 
 def eval_auc_check(model, device, n_impressions=4000, seed=11):
@@ -182,6 +182,37 @@ def _time_launches(fn, reps, device):
     return e0.elapsed_time(e1) / reps
 
 
+GEMM_CODES = {"f16x3": 2, "x6": 0, "f32": 1}   # nrms_gemm_arith_t
+
+
+def gemm_legs(model, cand, clk, mode, device, base, y_base):
+    """The timed step (nrms_forward, eager) under the other GEMM arithmetics:
+    ms / step, impressions / s, and the logits' distance to the default's
+    (the CPU-port distance is added after the cpu_baseline leg)."""
+    from newsrecommendationsystem_amd import _native as Nat
+    from newsrecommendationsystem_amd.pipeline import TimedForward
+    lib = Nat.load()
+    B = cand.shape[0]
+    legs = {}
+    for g in ("x6", "f32"):
+        if g == base:
+            continue
+        prev = lib.nrms_set_gemm_arith(GEMM_CODES[g])
+        try:
+            f = TimedForward(model, B, C, N_CLICKED, L, proj_mode=mode)
+            with torch.no_grad():
+                y = f.run(cand, clk).clone()
+                ms = _time_launches(lambda: f.run(cand, clk), 10, device)
+        finally:
+            lib.nrms_set_gemm_arith(prev)
+        legs[g] = {"ms_per_step": round(ms, 4), "impressions_per_s": round(B / (ms / 1e3), 1),
+                   "max_normwise_rel_err_vs_default": float(
+                       ((y - y_base).norm(dim=1) / y_base.norm(dim=1).clamp_min(1e-30)).max()),
+                   "timing": "eager nrms_forward calls, HIP events, 10 reps", "_logits": y}
+        del f
+    return legs
+
+
 def gather_hbm(device, V=1 << 20, n_titles=100_000, reps=20):
     """SURVEY §8d gather figure: nrms_embedding_gather alone over a 1.26 GB
     table (V = 1,048,576, beyond the 256 MB Infinity Cache), config-2 shape
@@ -200,10 +231,17 @@ def gather_hbm(device, V=1 << 20, n_titles=100_000, reps=20):
     nbytes = ids.numel() * (8 + 2 * 4 * D)
     gbs = nbytes / (ms / 1e3) / 1e9
     del table, out
-    return {"kernel": "gather_rows_kernel", "workload": f"{n_titles} titles x {L} tokens, V={V}, D={D}",
-            "bound": "hbm", "ms": round(ms, 4), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
-            "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": nbytes,
-            "traffic": load_traffic("gather"), "bit_exact_sample": ok}
+    traffic = load_traffic("gather")
+    out = {"kernel": "gather_rows_kernel", "workload": f"{n_titles} titles x {L} tokens, V={V}, D={D}",
+           "bound": "hbm", "ms": round(ms, 4), "achieved": round(gbs, 1), "peak": PEAK_HBM_GBS,
+           "unit": "GB/s", "frac": round(gbs / PEAK_HBM_GBS, 4), "bytes_per_launch": nbytes,
+           "traffic": traffic, "bit_exact_sample": ok}
+    if traffic:
+        # on the bytes that reached HBM (PMC): the padding rows (id 0) are served on-die
+        tgbs = traffic / (ms / 1e3) / 1e9
+        out["traffic_achieved"] = round(tgbs, 1)
+        out["frac_on_traffic"] = round(tgbs / PEAK_HBM_GBS, 4)
+    return out
 
 
 def news_encoder_cfg2(model, device, n_titles=100_000, reps=10):
@@ -240,18 +278,28 @@ def load_sq(kernel):
         return None
 
 
+# 16-bit products per fp32 product of each split arithmetic, per GEMM kind:
+# the Q|K|V projections (f16x3: A exact in 3 pieces, W in 2 -> 4 products),
+# the additive GEMMs (f16x3: 2 x 2 planes -> 3 products); x6: 6 everywhere
+PRODUCTS = {"f16x3": {"proj": 4, "additive": 3}, "x6": {"proj": 6, "additive": 6}, "f32": None}
+
+
 def issue_floor_ms(stage, w, gemm):
-    """Time the dominant stage's matrix / vector instructions need at the
-    MI355X peaks with nothing else in the way (SURVEY §8d FLOP split): the
-    x6 GEMM issues 6 bf16 products per fp32 product (2.5 PF dense), exact f32
-    MFMA and the attention contractions run at 157.3 TF, pooling on VALU."""
-    if stage != "news_fused":
+    """Time a stage's matrix / vector instructions need at the MI355X peaks
+    with nothing else in the way (the stage's FLOP split): split GEMMs issue
+    their 16-bit products at 2.5 PF dense, exact f32 MFMA, the attention
+    contractions and the pooling run at 157.3 TF (f32 MFMA = the vector rate);
+    the scorer is bound by its HBM bytes at 8 TB/s."""
+    if stage == "score":
+        return w["bytes"] / (PEAK_HBM_GBS * 1e9) * 1e3
+    f = w.get("split")
+    if f is None:
         return None
-    f = w["split"]
-    products = {"x6": 6, "f16x3": 3}.get(gemm)
-    gemm_s = (f["gemm"] * products / (PEAK_TFLOPS_BF16 * 1e12) if products
+    prod = PRODUCTS[gemm]
+    kind = "proj" if stage.startswith("qkv") else "additive"
+    gemm_s = (f["gemm"] * prod[kind] / (PEAK_TFLOPS_BF16 * 1e12) if prod
               else f["gemm"] / (PEAK_TFLOPS_F32 * 1e12))
-    rest_s = (f["attention"] + f["pool"]) / (PEAK_TFLOPS_F32 * 1e12)
+    rest_s = (f.get("attention", 0) + f.get("pool", 0)) / (PEAK_TFLOPS_F32 * 1e12)
     return (gemm_s + rest_s) * 1e3
 
 
@@ -284,6 +332,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend for the barrier / max-over-ranks timing (nccl = RCCL); "
                          "gloo lets several ranks share one GPU for a rehearsal")
+    ap.add_argument("--dump-logits", default=None, metavar="PATH",
+                    help="after the timed region, score every batch once more and save this rank's "
+                         "impression indices and logits to PATH.rank<r>.npz (multi-rank tests)")
     ap.add_argument("--gemm", choices=["f16x3", "x6", "f32"], default="f16x3",
                     help="GEMM arithmetic: split-f16 news additive GEMM and Q|K|V projections "
                          "(default), split-bf16 x6 everywhere, or exact f32 MFMA (all fp32-accurate)")
@@ -405,6 +456,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if args.dump_logits:
+        # untimed: every batch of this rank's shard once, logits by impression index
+        import numpy as np
+        with torch.no_grad():
+            ys = [fwd.run(*b).clone() for b in full] + ([tail_fwd.run(*tail[0]).clone()] if tail_fwd else [])
+        n_done = sum(y.shape[0] for y in ys)
+        np.savez(f"{args.dump_logits}.rank{rank}.npz", idx=idx[:n_done].cpu().numpy(),
+                 logits=torch.cat(ys).float().cpu().numpy())
     with torch.no_grad():
         run_steps(fwd, full, n_ev, events)
         torch.cuda.synchronize()
@@ -434,8 +493,10 @@ def main():
     n_clk = clk.shape[0] * N_CLICKED
     clk_pad = int(pad[:n_clk].sum())
     n_user = n_clk - max(clk_pad - 1, 0) if not args.unfused else n_clk
-    work = (plan.work(titles_encoded=n_enc, user_rows_projected=n_user, news_rows=news_rows)
-            if not args.unfused else plan.work())
+    # UserEncoder rows: every user on its N clicked positions
+    user_rows = (n_clk, clk.shape[0] * N_CLICKED * N_CLICKED)
+    work = (plan.work(titles_encoded=n_enc, user_rows_projected=n_user, news_rows=news_rows,
+                      user_rows=user_rows) if not args.unfused else plan.work())
     dom = max(stage_ms, key=stage_ms.get)
     w = work[dom]
     t_dom = stage_ms[dom] / 1e3
@@ -458,6 +519,13 @@ def main():
     else:
         value = world * B * steps / elapsed
     floor = issue_floor_ms(dom, w, args.gemm)
+    # every stage's instruction-level floor and the fraction of it achieved
+    stage_floor = {}
+    for st_name, ms in stage_ms.items():
+        if st_name in work:
+            fl = issue_floor_ms(st_name, work[st_name], args.gemm)
+            if fl is not None:
+                stage_floor[st_name] = {"floor_ms": round(fl, 4), "frac": round(fl / ms, 4)}
     sq = load_sq(dom)
     roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
                 "frac": round(achieved / peak, 4), "traffic": load_traffic(dom),
@@ -511,6 +579,12 @@ def main():
                                  "multiplicity (news_fused.hip; fp32-rounding-level difference: "
                                  "no_token_compaction below)"},
         "stages_ms": {st: round(v, 4) for st, v in stage_ms.items()},
+        "stages_issue_floor": stage_floor,
+        "stages_issue_floor_note": ("floor = the stage's algorithmic FLOP at the instruction rates it issues "
+                                    "(split GEMMs: their 16-bit products at 2.5 PF dense; attention / "
+                                    "pooling / exact f32 at 157.3 TF; the scorer: its bytes at 8 TB/s); "
+                                    "frac = floor / measured stage time"),
+        "user_rows_encoded": user_rows[0],
         "stages_note": f"HIP events recorded by the library between its stages, a separate pass of "
                        f"{n_ev} steps after the timed ones (events cost queue time, so the timed steps "
                        f"run without them)",
@@ -559,13 +633,30 @@ def main():
                 "note": "per-token Q|K|V projection (no vocabulary folding): the work SURVEY §8d's "
                         "789.6 MFLOP/impression unit describes"}
             del dfwd
+    legs = {}
+    if rank == 0 and world == 1 and not args.no_extras and not args.stream and not args.unfused:
+        # the same step in the other GEMM arithmetics: x6 (exact bf16 products,
+        # every operand split losslessly) beside the default's 22-bit operands
+        legs = gemm_legs(model, cand, clk, mode, device, args.gemm, y_fwd)
+        out["gemm_legs"] = legs
+    if rank == 0 and world == 1 and not args.no_extras and not args.stream:
+        # config 5's quality half (planted teacher): FedAvg on the HIP training
+        # path vs the CPU ATen path, both through evaluate()
+        from newsrecommendationsystem_amd import quality
+        out["fedavg_quality"] = quality.run(cpu=not args.no_cpu_baseline)
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.stream:
-        cb, parity = cpu_baseline(model, cand, clk)
+        cb, parity, ref_cpu = cpu_baseline(model, cand, clk)
         out["cpu_baseline"] = cb
         out["parity_vs_cpu"] = parity
+        for g, leg in legs.items():
+            yl = leg.pop("_logits").cpu()
+            leg["max_normwise_rel_err_vs_cpu"] = float(
+                ((yl - ref_cpu).norm(dim=1) / ref_cpu.norm(dim=1).clamp_min(1e-30)).max())
         out["auc_vs_cpu"] = eval_auc_check(model, device)
     else:
         out["cpu_baseline"] = None
+    for leg in legs.values():
+        leg.pop("_logits", None)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:

@@ -141,13 +141,14 @@ int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
                         hipStream_t s, float* wap = nullptr, bool* deduped = nullptr,
                         int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0,
-                        bool prepacked = false, bool direct_rows = false) {
+                        bool prepacked = false, bool direct_rows = false, bool* classified = nullptr) {
   const int D = w->d_model;
   if (deduped) *deduped = false;
+  if (classified) *classified = false;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
     return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
                              w->q_add, wap, out, s, -1, deduped, broadcast_from, user_list, user_rows,
-                             prepacked, direct_rows);
+                             prepacked, direct_rows, -1, classified);
   if (direct_rows) ids_a = ids_b = nullptr;   // per-token rows: the ids only classify (fused kernel)
   // stage kernels: any row stride >= 3D (packed rows, or the folded table's
   // padded 128-B-line rows that nrms_qkv_row_stride reports)
@@ -492,7 +493,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   };
 
   int32_t st;
-  bool deduped = false;
+  bool deduped = false, classified = false;
   const int arith = gemm_arith();
   const bool user_fused = fused_user_supported(N, D, user_w->n_heads, user_w->query_dim) &&
                           ((uintptr_t)user % 16) == 0;
@@ -524,7 +525,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
     if ((st = rec(1))) return st;
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
                          news, stream, wap, &deduped, bcast_from, user_rows_here ? ulist : nullptr, n_clk,
-                         prepacked);
+                         prepacked, false, &classified);
   } else {
     st = project_qkv(table, V, contiguous_rows(D), clicked_ids, n_clk * L, news_w, pack, packed, qkv, ld,
                      stream, nullptr, arith);
@@ -537,7 +538,8 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
     // titles' copies are written for every title, so the UserEncoder and the
     // scorer read plain rows)
     st = encode_from_qkv(qkv, ld, n_all * L, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx,
-                         scores, news, stream, wap, nullptr, 0, nullptr, 0, false, /*direct_rows=*/true);
+                         scores, news, stream, wap, nullptr, 0, nullptr, 0, false, /*direct_rows=*/true,
+                         &classified);
   }
   if (st) return st;
   if ((st = rec(2))) return st;

@@ -865,6 +865,10 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       // on its slot.
       {
         floatx4 acc[NB][3], accX = floatx4{0.f, 0.f, 0.f, 0.f}, accX2 = floatx4{0.f, 0.f, 0.f, 0.f};
+        // N-tile 12: this wave's M-tile xm (waves past NB compute an unused tile
+        // on M-tile 0), and M-tile 4 for wave 0 when NB = 5
+        const int xm = w < NB ? w : 0;
+        const bool extra = NB == 5 && w == 0;
 #pragma unroll
         for (int mt = 0; mt < NB; ++mt)
 #pragma unroll
@@ -886,51 +890,50 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
                 dst[j][pl] = __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(
                     brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
           };
-          // one 32-deep k-step; the wave index is a template constant (its N-tile
-          // 12 rows = M-tile W: no second read of them); A planes loaded lo
-          // first, the order the products consume them
-          auto kstep = [&](int ks, const bf16x8 (&bb)[4][3], auto wc) {
-            constexpr int W = decltype(wc)::value;
-            constexpr bool HASX = W < NB;
-            constexpr bool EXTRA = W == 0 && NB == 5;
-            bf16x8 a[NB][3];
+          // one 32-deep k-step, the same code for every wave (one copy per NB:
+          // wave-specialised copies made the kernel ~4x larger than the
+          // instruction cache); the N-tile-12 rows (M-tile xm) are read as
+          // their own fragments; A planes loaded lo first, the order the
+          // products consume them
+          auto kstep = [&](int ks, const bf16x8 (&bb)[4][3]) {
+            bf16x8 a[NB][3], ax[3];
 #pragma unroll
-            for (int pl = 2; pl >= 0; --pl)
+            for (int pl = 2; pl >= 0; --pl) {
 #pragma unroll
               for (int mt = 0; mt < NB; ++mt)
                 a[mt][pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * mt * XRB + pl * XKP + 32 * ks);
+              ax[pl] = *reinterpret_cast<const bf16x8*>(Ab + 16 * xm * XRB + pl * XKP + 32 * ks);
+            }
             // the six products with i + j <= 2, smallest first
 #define NRMS_X6STEP(PA, PB)                                                                              \
   _Pragma("unroll") for (int mt = 0; mt < NB; ++mt)                                                      \
   _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                          \
       acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);   \
-  if constexpr (HASX) accX = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[HASX ? W : 0][PA], bb[3][PB], accX, 0, 0, 0); \
-  if constexpr (EXTRA) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
+  accX = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ax[PA], bb[3][PB], accX, 0, 0, 0);                      \
+  if (extra) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
             NRMS_X6STEP(2, 0) NRMS_X6STEP(1, 1) NRMS_X6STEP(0, 2) NRMS_X6STEP(1, 0) NRMS_X6STEP(0, 1)
             NRMS_X6STEP(0, 0)
 #undef NRMS_X6STEP
           };
           // two B buffers in turn (XKS is even): no register copies between k-steps
-          auto mainloop = [&](auto wc) {
-            bf16x8 b0[4][3], b1[4][3];
-            load_b(0, b0);
+          bf16x8 b0[4][3], b1[4][3];
+          load_b(0, b0);
 #pragma unroll
-            for (int ks = 0; ks < XKS; ks += 2) {
-              load_b(ks + 1, b1);
-              kstep(ks, b0, wc);
-              __builtin_amdgcn_sched_barrier(0);
-              if (ks + 2 < XKS) load_b(ks + 2, b0);
-              kstep(ks + 1, b1, wc);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          };
-          static_assert(XKS % 2 == 0, "k-steps in pairs");
-          switch (w) {
-            case 0: mainloop(std::integral_constant<int, 0>{}); break;
-            case 1: mainloop(std::integral_constant<int, 1>{}); break;
-            case 2: mainloop(std::integral_constant<int, 2>{}); break;
-            default: mainloop(std::integral_constant<int, 3>{}); break;
+          for (int ks = 0; ks < XKS; ks += 2) {
+            // (each k-step's loads pinned ahead of the other buffer's MFMAs: left
+            // to the scheduler they sank among them and the next k-step waited
+            // for them -- with fewer M-tiles the k-step no longer covered the
+            // L2 latency)
+            load_b(ks + 1, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            kstep(ks, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + 2 < XKS) load_b(ks + 2, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            kstep(ks + 1, b1);
+            __builtin_amdgcn_sched_barrier(0);
           }
+          static_assert(XKS % 2 == 0, "k-steps in pairs");
         } else if constexpr (H3) {
           // products lo·hi, hi·lo, hi·hi' (each 2^11 x the true product) into acc
           const _Float16* Ah = ctxH + lm * XRH + 8 * kq;
@@ -952,49 +955,47 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
                 dst[j][pl] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(
                     brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
           };
-          auto kstep = [&](int ks, f16x8 (&bb)[4][3], auto wc) {
-            constexpr int W = decltype(wc)::value;
-            constexpr bool HASX = W < NB;
-            constexpr bool EXTRA = W == 0 && NB == 5;
+          // (one copy of the k-step for every wave, as the x6 path)
+          auto kstep = [&](int ks, f16x8 (&bb)[4][3]) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) bb[j][0] = bb[j][2] * (_Float16)kF16LoScale;
-            f16x8 a[NB][2];
+            f16x8 a[NB][2], ax[2];
 #pragma unroll
-            for (int pl = 1; pl >= 0; --pl)
+            for (int pl = 1; pl >= 0; --pl) {
 #pragma unroll
               for (int mt = 0; mt < NB; ++mt)
                 a[mt][pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * mt * XRH + pl * XKP + 32 * ks);
+              ax[pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * xm * XRH + pl * XKP + 32 * ks);
+            }
 #define NRMS_H3STEP(PA, PB)                                                                            \
   _Pragma("unroll") for (int mt = 0; mt < NB; ++mt)                                                    \
   _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                        \
       acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);  \
-  if constexpr (HASX) accX = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[HASX ? W : 0][PA], bb[3][PB], accX, 0, 0, 0); \
-  if constexpr (EXTRA) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
+  accX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ax[PA], bb[3][PB], accX, 0, 0, 0);                     \
+  if (extra) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
             NRMS_H3STEP(1, 2) NRMS_H3STEP(0, 1) NRMS_H3STEP(0, 0)
 #undef NRMS_H3STEP
           };
-          auto mainloop = [&](auto wc) {
-            f16x8 b0[4][3], b1[4][3];
-            load_b(0, b0);
-            // fully unrolled, each k-step's loads and MFMAs fenced in place
-            // (without the fences the scheduler hoists every load: 1,100 spills);
-            // a rolled loop permuted the accumulators at its back-edge (~170
-            // AGPR moves per iteration): 1.41 -> 1.33 ms
+          f16x8 b0[4][3], b1[4][3];
+          load_b(0, b0);
+          // fully unrolled, each k-step's loads and MFMAs fenced in place
+          // (without the fences the scheduler hoists every load: 1,100 spills);
+          // a rolled loop permuted the accumulators at its back-edge (~170
+          // AGPR moves per iteration): 1.41 -> 1.33 ms
 #pragma unroll
-            for (int ks = 0; ks < XKS; ks += 2) {
-              load_b(ks + 1, b1);
-              kstep(ks, b0, wc);
-              __builtin_amdgcn_sched_barrier(0);
-              if (ks + 2 < XKS) load_b(ks + 2, b0);
-              kstep(ks + 1, b1, wc);
-              __builtin_amdgcn_sched_barrier(0);
-            }
-          };
-          switch (w) {
-            case 0: mainloop(std::integral_constant<int, 0>{}); break;
-            case 1: mainloop(std::integral_constant<int, 1>{}); break;
-            case 2: mainloop(std::integral_constant<int, 2>{}); break;
-            default: mainloop(std::integral_constant<int, 3>{}); break;
+          for (int ks = 0; ks < XKS; ks += 2) {
+            // (each k-step's loads pinned ahead of the other buffer's MFMAs: left
+            // to the scheduler they sank among them and the next k-step waited
+            // for them -- with fewer M-tiles the k-step no longer covered the
+            // L2 latency)
+            load_b(ks + 1, b1);
+            __builtin_amdgcn_sched_barrier(0);
+            kstep(ks, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + 2 < XKS) load_b(ks + 2, b0);
+            __builtin_amdgcn_sched_barrier(0);
+            kstep(ks + 1, b1);
+            __builtin_amdgcn_sched_barrier(0);
           }
 #pragma unroll
           for (int mt = 0; mt < NB; ++mt)
@@ -1253,8 +1254,9 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting, bool* deduped,
                           int64_t broadcast_from, int64_t* user_list, int64_t user_rows, bool prepacked,
-                          bool direct_rows, int compact_setting) {
+                          bool direct_rows, int compact_setting, bool* classified) {
   if (deduped) *deduped = false;
+  if (classified) *classified = false;
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
   if (ldq < ROW || ldq % 4) return NRMS_ERR_UNSUPPORTED;   // float4 q / k slices
@@ -1335,6 +1337,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   }
   const int32_t st = launch_status();
   if (st == NRMS_OK && deduped) *deduped = dedupe;
+  if (st == NRMS_OK && classified) *classified = classify;
   return st;
 }
 

@@ -266,8 +266,10 @@ size_t fused_news_workspace_floats(int64_t n_titles);
 bool fused_news_supported(int L, int D, int H, int Q);
 // dedupe_setting / compact_setting: -1 = the process-wide setting
 // (nrms_set_title_dedupe / nrms_set_token_compaction), else 0 / 1; *deduped
-// (optional) tells whether the padding titles were classified
-// (fused_news_padding_groups is then valid until the workspace is reused).
+// (optional) tells whether the launch deduplicated the all-padding titles;
+// *classified (optional) whether it classified them at all (the pad_title
+// flags of fused_news_padding_groups are then valid until the workspace is
+// reused).
 // broadcast_from: the copies of the rep title's vector are written for titles
 // >= broadcast_from only. user_list (optional): when the launch deduplicates,
 // the main pass also builds launch_user_row_list's list of titles
@@ -280,7 +282,8 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr,
                           int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0,
-                          bool prepacked = false, bool direct_rows = false, int compact_setting = -1);
+                          bool prepacked = false, bool direct_rows = false, int compact_setting = -1,
+                          bool* classified = nullptr);
 PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles);
 // The rows m < n_rows of titles not copied from rep (the UserEncoder's rows to
 // project), appended to list in any order; their count in *pg.user_count.

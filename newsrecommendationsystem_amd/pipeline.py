@@ -132,24 +132,27 @@ class ForwardPlan:
 
     # Algorithmic work per launch of each stage (SURVEY §8d conventions:
     # GEMMs 2·M·N·K; bytes = operands the stage must read + results it writes).
-    def work(self, titles_encoded=None, user_rows_projected=None, news_rows=None):
+    def work(self, titles_encoded=None, user_rows_projected=None, news_rows=None, user_rows=None):
         """titles_encoded: titles the fused news tail actually encodes (with
         padding-title dedupe: the titles with a real token + one all-padding
         title); user_rows_projected: clicked rows the UserEncoder's Q|K|V GEMM
         projects (with dedupe: all but the copied padding rows); news_rows:
         (sum of Le, sum of Le^2) over the encoded titles, Le = the distinct q|k|v
         rows a title is encoded on (token compaction: real tokens + one padding
-        row; L without it); default all titles, L rows each."""
+        row; L without it); user_rows: (sum of Le, sum of Le^2) over the users
+        (UserEncoder compaction: real history positions + one padding row);
+        default all titles, L rows each, and N rows per user."""
         B, C, Nc, L, D, V = self.B, self.C, self.N, self.L, self.D, self.V
         Q, H, dk = 200, 15, D // 15
         n_all, n_clk = B * (C + Nc), B * Nc
         n_enc = n_all if titles_encoded is None else titles_encoded
         n_up = n_clk if user_rows_projected is None else user_rows_projected
         rows, rows_sq = (n_enc * L, n_enc * L * L) if news_rows is None else news_rows
+        urows, urows_sq = (n_clk, B * Nc * Nc) if user_rows is None else user_rows
         att_flop = lambda seqs, l: seqs * H * 2 * (2 * l * l * dk)
         qkv_m = V if self.folded else n_all * L
         return {
-            "qkv_news": dict(flop=2 * qkv_m * D * 3 * D,
+            "qkv_news": dict(flop=2 * qkv_m * D * 3 * D, split=dict(gemm=2 * qkv_m * D * 3 * D),
                              bytes=4 * (qkv_m * D + qkv_m * 3 * D + 3 * D * D)),
             # gathered q|k|v rows + ids + context rows written
             "mhsa_news": dict(flop=att_flop(n_all, L),
@@ -165,13 +168,16 @@ class ForwardPlan:
                                + 4 * (n_all * D + Q * D),
                                split=dict(attention=H * 4 * rows_sq * dk, gemm=2 * rows * D * Q,
                                           pool=2 * rows * D)),
-            "qkv_user": dict(flop=2 * n_up * D * 3 * D, bytes=4 * (n_up * 4 * D + 3 * D * D)),
+            "qkv_user": dict(flop=2 * n_up * D * 3 * D, bytes=4 * (n_up * 4 * D + 3 * D * D),
+                             split=dict(gemm=2 * n_up * D * 3 * D)),
             "mhsa_user": dict(flop=att_flop(B, Nc), bytes=4 * n_clk * 4 * D),
             "addscore_user": dict(flop=2 * n_clk * D * Q, bytes=4 * (n_clk * (D + 1) + Q * D)),
             "pool_user": dict(flop=2 * n_clk * D, bytes=4 * (n_clk * (D + 1) + B * D)),
             # fused user tail: q|k|v rows in, user vectors out (context stays in LDS)
-            "user_fused": dict(flop=att_flop(B, Nc) + 2 * n_clk * D * Q + 2 * n_clk * D,
-                               bytes=4 * (n_clk * 3 * D + B * D + Q * D)),
+            "user_fused": dict(flop=H * 4 * urows_sq * dk + 2 * urows * D * Q + 2 * urows * D,
+                               bytes=4 * (urows * 3 * D + B * D + Q * D),
+                               split=dict(attention=H * 4 * urows_sq * dk, gemm=2 * urows * D * Q,
+                                          pool=2 * urows * D)),
             "score": dict(flop=2 * B * C * D, bytes=4 * (B * C * D + B * D + B * C)),
         }
 

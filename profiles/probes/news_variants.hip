@@ -47,8 +47,9 @@ int main(int argc, char** argv) {
   for (auto& v : h_b) v = (rnd() - 0.5f) * 0.1f;
   for (auto& v : h_q) v = (rnd() - 0.5f) * 0.2f;
   // titles of the bench's stream: length U{5..20}, right-padded with id 0
+  const int fixed_len = getenv("NV_LEN") ? atoi(getenv("NV_LEN")) : 0;   // every title this long
   for (int64_t s = 0; s < n_titles; ++s) {
-    const int len = 5 + (int)(rnd() * 16);
+    const int len = fixed_len ? fixed_len : 5 + (int)(rnd() * 16);
     for (int t = 0; t < 20; ++t) h_ids[s * 20 + t] = t < len ? 1 + (int64_t)(rnd() * id_range) : 0;
   }
   for (int t = 0; t < 20; ++t) h_ids[7 * 20 + t] = 0;   // an all-padding title

@@ -4,7 +4,7 @@ MASTER_PORT in the environment), all ranks on cuda:0, collectives on gloo
 (RCCL cannot put two ranks on one GPU). Writes its results as .npy / .json
 files into the output directory given on the command line.
 
-    python tests/mp_gpu_worker.py eval|fedavg OUT_DIR
+    python tests/mp_gpu_worker.py eval|fedavg|quality OUT_DIR
 """
 import json
 import os
@@ -85,13 +85,41 @@ def run_fedavg(rank, world, out):
         json.dump({"losses": losses, "synced": synced, "optimizer": type(opt).__name__}, f)
 
 
+def run_quality(rank, world, out):
+    """Config 5 quality (newsrecommendationsystem_amd/quality.py): this rank is
+    one FedAvg client on the HIP path (HIP training kernels + HipAdam, the
+    parameter all-reduce of train.FedAvg over the process group), from the
+    initialisation and batches the test wrote; rank 0 saves the result."""
+    from newsrecommendationsystem_amd import quality as Q
+    from newsrecommendationsystem_amd import train as TR
+    from newsrecommendationsystem_amd.nrms import NRMS
+    meta = json.load(open(os.path.join(out, "quality_meta.json")))
+    cfg = Q.make_config(meta["V"], meta["lr"])
+    m = NRMS(cfg)
+    init = torch.load(os.path.join(out, "init.pt"), weights_only=True)
+    m.load_state_dict(init)
+    m = m.to("cuda:0")
+    opt = TR.make_optimizer(m)
+    fed = TR.FedAvg(m, every=meta["every"])
+    b = np.load(os.path.join(out, f"batches{rank}.npz"))
+    for k in range(b["cand"].shape[0]):
+        cand = torch.from_numpy(b["cand"][k]).to("cuda:0")
+        clk = torch.from_numpy(b["clk"][k]).to("cuda:0")
+        TR.train_step(m, opt, cand, clk)
+        fed.step()
+    if rank == 0:
+        torch.save({k: v.detach().cpu() for k, v in m.state_dict().items()}, os.path.join(out, "hip_fedavg.pt"))
+    with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        json.dump({"steps": int(b["cand"].shape[0]), "optimizer": type(opt).__name__}, f)
+
+
 def main():
     mode, out = sys.argv[1], sys.argv[2]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        {"eval": run_eval, "fedavg": run_fedavg}[mode](rank, world, out)
+        {"eval": run_eval, "fedavg": run_fedavg, "quality": run_quality}[mode](rank, world, out)
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -89,3 +89,79 @@ def test_fedavg_hip_training_two_ranks(tmp_path):
     mean = (pre[0] + pre[1]) / np.float32(2)
     assert np.array_equal(post[0], mean.astype(np.float32))
     assert all(np.isfinite(r["losses"]).all() for r in res)
+
+
+@pytest.mark.timeout(900)
+def test_bench_two_ranks_stream_matches_one_rank(tmp_path):
+    """The multi-rank bench path the driver's SCALE run takes (bench.py under
+    torch.distributed.run, one process per rank, user-sharded config-4 stream;
+    here gloo and both ranks on cuda:0): rc 0, exactly one JSON line (rank 0),
+    the two shards together score every impression of the stream once, and
+    every impression's logits equal the single-rank run's bitwise (the batch
+    an impression lands in never changes its logits)."""
+    n = 20000
+    common = ["--stream", "--stream-impressions", str(n), "--no-extras", "--no-cpu-baseline", "--warmup", "1"]
+    one = subprocess.run([sys.executable, "-u", "bench.py", *common, "--dump-logits", str(tmp_path / "one")],
+                         cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert one.returncode == 0, one.stderr[-3000:]
+    port = _free_port()
+    two = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+                          "--dist-backend", "gloo", *common, "--dump-logits", str(tmp_path / "two")],
+                         cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert two.returncode == 0, two.stderr[-3000:]
+    lines = [ln for ln in two.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, two.stdout[-3000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2 and rec["scaling"] == "strong" and rec["value"] > 0
+    ref = np.load(tmp_path / "one.rank0.npz")
+    assert np.array_equal(ref["idx"], np.arange(n))
+    parts = [np.load(tmp_path / f"two.rank{r}.npz") for r in range(2)]
+    idx = np.concatenate([p["idx"] for p in parts])
+    assert len(idx) == n and np.array_equal(np.sort(idx), np.arange(n))
+    assert len(set(parts[0]["idx"].tolist()) & set(parts[1]["idx"].tolist())) == 0
+    logits = np.concatenate([p["logits"] for p in parts])
+    assert np.isfinite(logits).all()
+    assert np.array_equal(logits.view(np.uint32), ref["logits"][idx].view(np.uint32))
+
+
+@pytest.mark.timeout(600)
+def test_fedavg_training_quality_hip_vs_cpu(tmp_path):
+    """Config 5's AUC half on a planted teacher (SURVEY §8d fallback; MIND is
+    absent): two FedAvg clients on the HIP path (two processes on the GPU,
+    HIP training kernels + HipAdam, train.FedAvg's all-reduce over gloo)
+    against the same schedule on the CPU ATen path (train.py + torch Adam),
+    from one initialisation, dropout 0; both evaluated with evaluate() on the
+    teacher-labelled split: |AUC_hip - AUC_cpu| <= 0.002, and training moved
+    the AUC away from the initial model's."""
+    import torch
+    from newsrecommendationsystem_amd import quality as Q
+    steps, every, B = 32, 4, 16
+    d = tmp_path / "split"
+    cfg, teacher, corpus, titles, student = Q.setup(str(d))
+    batches = [Q.teacher_batches(teacher, titles, 100 + 17 * r, steps, B) for r in range(2)]
+    for r, bs in enumerate(batches):
+        np.savez(tmp_path / f"batches{r}.npz", cand=np.stack([c.numpy() for c, _ in bs]),
+                 clk=np.stack([k.numpy() for _, k in bs]))
+    torch.save(student.state_dict(), tmp_path / "init.pt")
+    with open(tmp_path / "quality_meta.json", "w") as f:
+        json.dump({"V": cfg.num_words, "lr": cfg.learning_rate, "every": every}, f)
+    res = _run("quality", tmp_path, timeout=400)
+    assert all(r["optimizer"] == "HipAdam" and r["steps"] == steps for r in res)
+    hip_sd = torch.load(tmp_path / "hip_fedavg.pt", weights_only=True)
+    cpu_m, _, _ = Q.train_clients(student, batches, every, torch.device("cpu"))
+    cpu_sd = {k: v.detach() for k, v in cpu_m.state_dict().items()}
+    a_init = Q.auc_of(student.state_dict(), cfg, str(d))[0]
+    a_hip = Q.auc_of(hip_sd, cfg, str(d))[0]
+    a_cpu = Q.auc_of(cpu_sd, cfg, str(d))[0]
+    assert abs(a_hip - a_cpu) <= 0.002, (a_hip, a_cpu)
+    assert abs(a_hip - a_init) > 0.005, (a_init, a_hip)   # training moved it (0.574 -> 0.585 measured)
+    for k in cpu_sd:
+        if k.endswith("W_K.bias"):
+            # its gradient is analytically zero (a key bias adds q . b_K to every
+            # score of a query, which the normalisation divides out): Adam turns
+            # the rounding noise of either path into +-lr steps, so the two
+            # trajectories of this parameter are not comparable
+            continue
+        rel = float((hip_sd[k] - cpu_sd[k]).norm() / cpu_sd[k].norm().clamp_min(1e-30))
+        assert rel < 1e-3, (k, rel)

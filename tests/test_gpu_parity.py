@@ -851,6 +851,14 @@ def test_token_compaction_forward_vs_oracle(device, gemm_mode):
     sd = W.nrms_state(73, V)
     m = _module(sd, V, device, hip_proj_mode=N.NRMS_PROJ_FOLDED)
     cand, clk, _ = W.impressions(73, 9, B, V)
+    cand, clk = cand.copy(), clk.copy()
+    # UserEncoder compaction buckets (Le = real + 1 <= 16 / 32 / 50) at their
+    # edges: history lengths 1, 15, 16, 31, 32, 49, 50 (no padding row)
+    full, _, _ = W.impressions(74, 9, 7, V)
+    full_clk = W.titles(74, 31, 7 * 50, V).reshape(7, 50, 20)
+    for b, h in enumerate([1, 15, 16, 31, 32, 49, 50]):
+        clk[b] = full_clk[b]
+        clk[b, : 50 - h] = 0
     lib = N.load()
     ys = {}
     prev = lib.nrms_set_token_compaction(1)
