@@ -267,6 +267,17 @@ size_t nrms_user_attention_pool_workspace_size(int64_t B, int32_t N, int32_t D);
 int32_t nrms_user_attention_pool(const float* qkv, int64_t ld_qkv, int64_t B, int32_t N,
                                  const nrms_encoder_weights_t* w, float* out, void* workspace,
                                  size_t workspace_bytes, hipStream_t stream);
+/* The same with pad_flags[B * N] (uint8, non-zero: position b*N + i holds an
+ * all-padding title, src/dataset.py:79-83 -- all such positions carry one
+ * news vector, so their qkv rows are equal). With token compaction on
+ * (nrms_set_token_compaction) each user is encoded on its distinct rows: the
+ * padding positions collapse into one row, counted once per position in the
+ * raw-exp sums (bitwise the uncompacted sums for left padding), the context
+ * and the softmax / pooling (fp32-rounding-level difference); nrms_forward
+ * does the same. Off: as nrms_user_attention_pool. */
+int32_t nrms_user_attention_pool_padded(const float* qkv, int64_t ld_qkv, int64_t B, int32_t N,
+                                        const uint8_t* pad_flags, const nrms_encoder_weights_t* w, float* out,
+                                        void* workspace, size_t workspace_bytes, hipStream_t stream);
 
 /* DotProductClickPredictor.forward (src/model/general/click_predictor/
  * dot_product.py:8-19): out[b, c] = <news[b*stride_b + c*stride_c, :], user[b*stride_u, :]>,

@@ -62,6 +62,7 @@ SIGNATURES = {
     "nrms_news_encode_folded": (_i32, [_p, _i64, _i32, _p, _i64, _i64, _EW, _p, _p, _sz, _p]),
     "nrms_user_attention_pool_workspace_size": (_sz, [_i64, _i32, _i32]),
     "nrms_user_attention_pool": (_i32, [_p, _i64, _i64, _i32, _EW, _p, _p, _sz, _p]),
+    "nrms_user_attention_pool_padded": (_i32, [_p, _i64, _i64, _i32, _p, _EW, _p, _p, _sz, _p]),
     "nrms_user_encode_workspace_size": (_sz, [_i64, _i32, _i32]),
     "nrms_user_encode": (_i32, [_p, _i64, _i32, _i64, _i64, _EW, _p, _p, _sz, _p]),
     "nrms_score": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p]),

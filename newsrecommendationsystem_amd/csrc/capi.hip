@@ -390,6 +390,24 @@ int32_t nrms_user_attention_pool(const float* qkv, int64_t ld_qkv, int64_t B, in
   return launch_fused_user(qkv, ld_qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream);
 }
 
+int32_t nrms_user_attention_pool_padded(const float* qkv, int64_t ld_qkv, int64_t B, int32_t N,
+                                        const uint8_t* pad_flags, const nrms_encoder_weights_t* w, float* out,
+                                        void* workspace, size_t workspace_bytes, hipStream_t stream) {
+  if (B < 0 || N <= 0) return NRMS_ERR_INVALID_ARG;
+  if (int32_t st = shape_ok(w)) return st;
+  if (!fused_user_supported(N, w->d_model, w->n_heads, w->query_dim)) return NRMS_ERR_UNSUPPORTED;
+  if (B == 0) return NRMS_OK;
+  if (!qkv || !out || !pad_flags) return NRMS_ERR_INVALID_ARG;
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* wap = cv.floats(fused_user_packed_b_floats());
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
+  if (ld_qkv == 0) ld_qkv = 3 * (int64_t)w->d_model;
+  const bool compact = token_compaction() && N <= 64;
+  const PaddingGroups pg{pad_flags, nullptr, nullptr};   // (no rep: every flagged row was projected)
+  return launch_fused_user(qkv, ld_qkv, B, N, w->w_add, w->b_add, w->q_add, wap, out, stream,
+                           compact ? &pg : nullptr, false, false, compact);
+}
+
 int32_t nrms_user_encode(const float* clicked, int64_t B, int32_t N, int64_t stride_b,
                          int64_t stride_n, const nrms_encoder_weights_t* w, float* out,
                          void* workspace, size_t workspace_bytes, hipStream_t stream) {
@@ -564,9 +582,14 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   }
   if (st) return st;
   if ((st = rec(3))) return st;
+  // UserEncoder token compaction (user_fused.hip): a user's padding positions
+  // (one news vector) collapse into one row carrying their count
+  const bool user_compact = user_fused && classified && token_compaction() && N <= 64;
+  const PaddingGroups pg_flags = classified ? fused_news_padding_groups(wap, n_all) : pg;
   if (user_fused)
     st = launch_fused_user(uqkv, uld, B, N, user_w->w_add, user_w->b_add, user_w->q_add, uwap, user,
-                           stream, user_dedupe ? &pg : nullptr, prepacked);
+                           stream, (user_dedupe || user_compact) ? &pg_flags : nullptr, prepacked, user_dedupe,
+                           user_compact);
   else
     st = encode_from_qkv(uqkv, uld, n_clk, nullptr, B, nullptr, B, N, user_w, uctx, uscores, user,
                          stream);

@@ -244,11 +244,15 @@ struct PaddingGroups {
 };
 size_t fused_user_packed_b_floats();
 bool fused_user_supported(int L, int D, int H, int Q);
-// pg (optional): rows m = b L + i of copied padding titles (see
-// PaddingGroups) are read from row *rep.
+// pg (optional): the clicked titles' padding flags. copied: rows m = b L + i
+// of copied padding titles (see PaddingGroups) were not projected and are read
+// from row *rep. compact (L <= 64): each user is encoded on its distinct rows,
+// its padding positions collapsed into one row with their count
+// (user_fused.hip).
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
-                          hipStream_t s, const PaddingGroups* pg = nullptr, bool prepacked = false);
+                          hipStream_t s, const PaddingGroups* pg = nullptr, bool prepacked = false,
+                          bool copied = false, bool compact = false);
 // Process-wide switch (news_fused.hip): encode one all-padding title per
 // batch and broadcast its vector (nrms_set_title_dedupe; NRMS_DEDUPE=0 in the
 // environment turns it off).

@@ -89,11 +89,23 @@ __device__ __forceinline__ int ukpos(int k) {
   return (k & ~31) + 8 * ((k & 15) >> 2) + 4 * ((k & 31) >> 4) + (k & 3);
 }
 
+// Token compaction (uflags & UF_COMPACT, nrms_forward): the clicked positions
+// of a user whose titles are all padding (the left-padding of short
+// histories, src/dataset.py:79-83) have one news vector, so wave 0 lists the
+// user's Le = real + 1 distinct rows -- the padding row first, the real
+// positions in order -- and the whole tail runs on Le rows, the padding row
+// counted n_pad times: its exp added n_pad times first in every raw-exp sum
+// (the reference's key order for left padding: the sums are bitwise the
+// uncompacted ones), its attention weight and its softmax weight scaled by
+// n_pad. UF_COPIED: the copied padding titles' rows were not projected (the
+// row-list projection after dedupe); the padding row is then rep's, else the
+// user's own first padding position's.
+constexpr int UF_COPIED = 1, UF_COMPACT = 2;
 template <int MODE, int LMAX, int NT>
 __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
-    const float* __restrict__ qkv, int64_t ldq, int L, const float* __restrict__ WaP,
+    const float* __restrict__ qkv, int64_t ldq, int L_all, const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
-    PaddingGroups pg) {
+    PaddingGroups pg, int uflags) {
   static_assert(NT >= UH * LMAX, "one (head, query) task per thread");
   constexpr int NW = NT / 64;
   constexpr int NTPW = (UNT + NW - 1) / NW;            // N-tiles per wave
@@ -121,8 +133,32 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // q|k|v row of position i (stride ldq floats); with pg, a position holding a
   // copied padding title reads the row of the title it copies
-  const int32_t rep = pg.pad_title ? *pg.rep : 0;
+  const int32_t rep = (pg.pad_title && pg.rep) ? *pg.rep : 0;   // (no rep: the padded stage entry)
+  const bool compact = (uflags & UF_COMPACT) != 0;
+  __shared__ int32_t urow[LMAX + 1];   // compacted rows, then n_pad
+  int L = L_all, m0 = 1;               // rows of this user; times row 0 counts
+  if (compact) {
+    static_assert(LMAX <= 64, "one lane per history position");
+    if (w == 0) {
+      const int64_t base = s * L_all;
+      const bool padp = lane < L_all && pg.pad_title[base + lane];
+      const uint64_t pm = __ballot(padp);
+      const uint64_t real = __ballot(lane < L_all && !padp);
+      const int npad = __popcll(pm);
+      const int lead = npad > 0 ? 1 : 0;
+      if (lane < L_all && !padp) urow[lead + __popcll(real & ((1ull << lane) - 1))] = (int32_t)(base + lane);
+      if (lane == 0) {
+        if (npad) urow[0] = (uflags & UF_COPIED) ? rep : (int32_t)(base + __ffsll((long long)pm) - 1);
+        urow[LMAX] = npad;
+      }
+    }
+    __syncthreads();
+    const int npad = urow[LMAX];
+    L = L_all - npad + (npad > 0 ? 1 : 0);
+    m0 = npad > 1 ? npad : 1;
+  }
   auto row = [&](int i) -> const float* {
+    if (compact) return qkv + (int64_t)urow[i] * ldq;
     int64_t m = s * L + i;
     if (pg.pad_title && pg.pad_title[m] && m != rep) m = rep;
     return qkv + m * ldq;
@@ -195,7 +231,10 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     for (int j = 0; j < LMAX; ++j) {
       const float x = raw(j);
       if constexpr (kKeep) e[j] = x;
-      sum += x;
+      if (j == 0)
+        for (int c = 0; c < m0; ++c) sum += x;   // (row 0's multiplicity, one addition at a time)
+      else
+        sum += x;
     }
     if (exp_row_needs_recheck(sum)) {   // rare: rows near fp32 overflow
       exact = true;
@@ -204,7 +243,10 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       for (int j = 0; j < LMAX; ++j) {
         const float x = raw_exact(j);
         if constexpr (kKeep) e[j] = x;
-        sum += x;
+        if (j == 0)
+          for (int c = 0; c < m0; ++c) sum += x;
+        else
+          sum += x;
       }
     }
     const float inv = 1.0f / (sum + 1e-8f);
@@ -215,7 +257,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       const int jj = j < L ? j : L - 1;
       float ej;
       if constexpr (kKeep) ej = e[j]; else ej = exact ? raw_exact(j) : raw(j);
-      const float a = ej * inv;
+      float a = ej * inv;
+      if (j == 0 && m0 > 1) a *= (float)m0;
       const float4* vr = reinterpret_cast<const float4*>(tile + jj * URS + UD + UDK * h);
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
@@ -433,7 +476,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       for (int nt = 1; nt < UNT; ++nt) v += part[nt * 64 + lane];
     }
     const float mx = wave_max_nan(v);
-    const float ex = lane < L ? expf(v - mx) : 0.f;
+    float ex = lane < L ? expf(v - mx) : 0.f;
+    if (lane == 0 && m0 > 1) ex *= (float)m0;
     wts[lane] = ex / wave_sum(ex);
   }
   __syncthreads();
@@ -493,22 +537,22 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 template <int MODE, int LMAX, int NT>
 int32_t launch_user_inst(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
-                         PaddingGroups pg) {
+                         PaddingGroups pg, int uflags) {
   const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64 + 2 * 64) * 4;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>), (int)lds);
   hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
-                     ldq, L, wap, b_add, q_add, out, pg);
+                     ldq, L, wap, b_add, q_add, out, pg, uflags);
   return launch_status();
 }
 
 template <int MODE>
 int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
-                         PaddingGroups pg) {
-  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
-  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
-  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
-  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
+                         PaddingGroups pg, int uflags) {
+  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
+  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
+  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
+  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
 }
 
 }  // namespace
@@ -521,8 +565,11 @@ bool fused_user_supported(int L, int D, int H, int Q) {
 
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
-                          hipStream_t s, const PaddingGroups* pgp, bool prepacked) {
+                          hipStream_t s, const PaddingGroups* pgp, bool prepacked, bool copied, bool compact) {
   const PaddingGroups pg = pgp ? *pgp : PaddingGroups{nullptr, nullptr, nullptr};
+  if (compact && (!pgp || L > 64 || B * L > INT32_MAX)) return NRMS_ERR_UNSUPPORTED;
+  if (copied && !pgp) return NRMS_ERR_INVALID_ARG;
+  const int uflags = (copied ? UF_COPIED : 0) | (compact ? UF_COMPACT : 0);
   if (B == 0) return NRMS_OK;
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16 || ldq < 3 * UD || ldq % 4)
@@ -534,9 +581,9 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
     hipLaunchKernelGGL(pack_user_b_kernel, dim3(blocks), dim3(256), 0, s, w_add, wap, mode);
     if (int32_t st = launch_status()) return st;
   }
-  if (mode == 2) return launch_user_mode<2>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
-  if (mode == 1) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
-  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg);
+  if (mode == 2) return launch_user_mode<2>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
+  if (mode == 1) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
+  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
 }
 
 }  // namespace nrms

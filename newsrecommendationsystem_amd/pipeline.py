@@ -113,7 +113,10 @@ class ForwardPlan:
         N.call("nrms_qkv_project_ws", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), uldq, pws, npws, st)
         rec(k + 1)
         if self.user_fused:
-            N.call("nrms_user_attention_pool", P(self.uqkv), uldq, B, Nc, wu, P(self.user),
+            # the clicked positions holding all-padding titles (one news vector):
+            # the tail compacts them as nrms_forward does (token compaction)
+            pad = (clicked_ids == 0).all(-1).to(torch.uint8).contiguous()
+            N.call("nrms_user_attention_pool_padded", P(self.uqkv), uldq, B, Nc, P(pad), wu, P(self.user),
                    P(self.uws), self.uws.numel(), st)
             k += 1
         else:

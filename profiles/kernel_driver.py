@@ -28,6 +28,19 @@ def main():
     ap.add_argument("--unfused", action="store_true")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
+    if a.stage == "forward":   # the product path itself (nrms_forward on the bench's stream batch)
+        from newsrecommendationsystem_amd import stream as S
+        from newsrecommendationsystem_amd.pipeline import TimedForward
+        model = bench.build_model(dev)
+        idx = bench.stream_impressions(0, 1, 1024, dev)
+        cand, clk = S.batch(0, idx, bench.V_WORDS)
+        fwd = TimedForward(model, 1024, bench.C, bench.N_CLICKED, bench.L)
+        with torch.no_grad():
+            for _ in range(a.iters + 1):
+                fwd.run(cand, clk)
+        torch.cuda.synchronize()
+        print("ok", a.stage, a.iters)
+        return
     if a.stage == "gather":   # isolated HBM gather figure (bench.gather_hbm)
         for _ in range(a.iters):
             bench.gather_hbm(dev, reps=1)

@@ -19,7 +19,7 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o gather -- python3 "${GATHER[@]}"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o gather -- python3 "${GATHER[@]}"
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o gather -- python3 "${GATHER[@]}"
-# SQ counters of the dominant kernels (bench.py roofline.sq_counters)
-bash "$REPO/profiles/counters.sh" news_fused "$TAG"
-bash "$REPO/profiles/counters.sh" qkv_news "$TAG"
+# SQ counters of every stage's kernel, from passes over the product path
+# itself (nrms_forward on the bench batch): bench.py roofline.sq_counters
+bash "$REPO/profiles/counters.sh" forward "$TAG"
 find "$OUT" -name '*.csv' | sort

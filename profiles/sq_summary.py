@@ -16,11 +16,12 @@ import sys
 from collections import defaultdict
 
 KERNELS = {"news_fused": "fused_news_kernel", "qkv_news": "proj_qkv_kernel<false",
-           "qkv_user": "proj_qkv_kernel", "user_fused": "fused_user_kernel",
+           "qkv_user": "proj_qkv_kernel<true", "user_fused": "fused_user_kernel",
            "qkv_news_staged": "gemm_x6_kernel"}
 
 
 def main():
+    # (several stages may be read from one pass over the whole forward)
     d, stage, tag = sys.argv[1], sys.argv[2], sys.argv[3]
     acc = defaultdict(lambda: defaultdict(list))
     for f in glob.glob(os.path.join(d, "*", "run_counter_collection.csv")):

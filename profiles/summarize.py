@@ -37,7 +37,7 @@ def stage_of(name, grid_threads, wg):
         return "pack_add_news"
     if "pack_user_b" in name:
         return "pack_add_user"
-    if "classify_groups" in name:
+    if "classify_groups" in name or "classify_titles" in name:
         return "classify"
     if "broadcast_padding" in name:
         return "broadcast"

@@ -667,6 +667,69 @@ def test_fused_user_tail_vs_stages(device, B, n_clk, gemm_mode):
     assert torch.equal(u, out)
 
 
+@pytest.mark.parametrize("B,n_clk", [(40, 50), (9, 17), (6, 64)])
+def test_user_tail_padded_compaction(device, B, n_clk, gemm_mode):
+    """nrms_user_attention_pool_padded: the clicked positions flagged as
+    all-padding titles (one news vector) collapse into one row with their
+    count. Histories with 0, 1, some, all-but-one and all positions padding,
+    left-padded and interleaved: within fp32 rounding of the uncompacted tail
+    (nrms_user_attention_pool) and of the fp64 oracle; with token compaction
+    off it is the uncompacted tail bitwise."""
+    from newsrecommendationsystem_amd import _native as N
+    V = 300
+    sd = W.nrms_state(29, V)
+    m = _module(sd, V, device)
+    rng = np.random.default_rng(200 + n_clk)
+    vec = (0.3 * rng.standard_normal((B, n_clk, 300))).astype(np.float32)
+    padv = (0.3 * rng.standard_normal(300)).astype(np.float32)   # the padding title's vector
+    flags = np.zeros((B, n_clk), np.uint8)
+    for b in range(B):
+        kind = b % 6
+        if kind == 1:
+            flags[b, :1] = 1
+        elif kind == 2:
+            flags[b, : rng.integers(1, n_clk)] = 1          # left padding
+        elif kind == 3:
+            flags[b, : n_clk - 1] = 1
+        elif kind == 4:
+            flags[b, :] = 1
+        elif kind == 5:
+            flags[b, rng.random(n_clk) < 0.4] = 1           # interleaved
+    vec[flags.astype(bool)] = padv
+    x = torch.from_numpy(vec).to(device).reshape(B * n_clk, 300).contiguous()
+    w, keep = m.user_encoder.weights()
+    st = N.stream_handle(device)
+    lib = N.load()
+    uqkv = torch.empty(B * n_clk, 900, device=device)
+    pb = lib.nrms_qkv_project_workspace_size(300)
+    pws = torch.empty(pb, dtype=torch.uint8, device=device)
+    N.call("nrms_qkv_project_ws", N.ptr(x), B * n_clk, None, B * n_clk, ctypes.byref(w), N.ptr(uqkv), 0,
+           N.ptr(pws), pb, st)
+    nb = lib.nrms_user_attention_pool_workspace_size(B, n_clk, 300)
+    ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    fl = torch.from_numpy(flags.reshape(-1)).to(device)
+    plain = torch.empty(B, 300, device=device)
+    N.call("nrms_user_attention_pool", N.ptr(uqkv), 0, B, n_clk, ctypes.byref(w), N.ptr(plain),
+           N.ptr(ws), nb, st)
+    outs = {}
+    prev = lib.nrms_set_token_compaction(1)
+    try:
+        for on in (1, 0):
+            lib.nrms_set_token_compaction(on)
+            o = torch.empty(B, 300, device=device)
+            N.call("nrms_user_attention_pool_padded", N.ptr(uqkv), 0, B, n_clk, N.ptr(fl), ctypes.byref(w),
+                   N.ptr(o), N.ptr(ws), nb, st)
+            outs[on] = o
+    finally:
+        lib.nrms_set_token_compaction(prev)
+    assert torch.equal(outs[0], plain)
+    assert torch.isfinite(outs[1]).all()
+    err = ((outs[1] - plain).norm(dim=1) / plain.norm(dim=1)).max()
+    assert err < 2e-6, float(err)
+    oracle = O.user_encode(vec, sd, np.float64)
+    assert O.normwise_rel_err(_np(outs[1]), oracle).max() < 1e-5
+
+
 def test_fused_user_tail_value_range(device, gemm_mode):
     """The fused UserEncoder tail with V rows from 1e-20 to 1e25 in magnitude
     (per user; Q and K small, so the raw exps stay finite): the split-f16
