@@ -169,6 +169,58 @@ def eval_auc_check(model, device, n_impressions=4000, seed=11):
             "labels": "planted teacher (Bernoulli(sigmoid(model logit)))"}
 
 
+def eval_throughput(model, device, seed=5):
+    """evaluate() impressions/s on a synthetic split of MIND-small-dev's shape
+    (73,152 impressions, 42,416 news, 50,000 users, U{2..73} candidates per
+    impression; uniform p = 0.2 labels), the host stages (reading the two TSV
+    files, building the EvalPlan) timed apart from the GPU passes (news
+    vectors, user vectors, the score_pairs and impression_metrics launches,
+    the nanmean) -- src/evaluate.py:171-272's whole job."""
+    import tempfile
+    from newsrecommendationsystem_amd import data as Dt
+    from newsrecommendationsystem_amd import evaluate as EV
+    shape = dict(n_news=42416, n_users=50000, n_impressions=73152, V=V_WORDS, min_cands=2, max_cands=73)
+
+    def clock():
+        torch.cuda.synchronize(device)
+        return time.perf_counter()
+
+    with tempfile.TemporaryDirectory() as d:
+        Dt.synthetic_split(d, seed=seed, **shape)
+        t0 = clock()
+        corpus = Dt.read_news_parsed(os.path.join(d, "news_parsed.tsv"))
+        imps = Dt.read_behaviors(os.path.join(d, "behaviors.tsv"))
+        t1 = clock()
+        plan = EV.EvalPlan(corpus, imps, num_clicked=model.config.num_clicked_news_a_user)
+        t2 = clock()
+        with torch.no_grad():
+            tab = EV.news_vectors(model, plan.corpus.titles)
+            t3 = clock()
+            users = EV.user_vectors(model, tab, plan.hist_rows)
+            t4 = clock()
+            del tab, users
+            _, metrics = EV.score_plan(model, plan)   # (all passes again, for the total)
+            means = EV.reduce_means(*EV.nan_sums(metrics))
+        t5 = clock()
+        t_e0 = clock()
+        again = EV.evaluate(model, d)
+        t_e1 = clock()
+    n = plan.n_impressions
+    return {
+        "workload": "synthetic split of MIND-small-dev shape: 73,152 impressions, 42,416 news, "
+                    "50,000 users, U{2..73} candidates, U{0..70} clicked (first 50 kept)",
+        "impressions": n, "candidates": int(plan.cand.shape[0]), "distinct_histories": int(plan.hist_rows.shape[0]),
+        "host_read_s": round(t1 - t0, 3), "host_plan_s": round(t2 - t1, 3),
+        "gpu_news_vectors_s": round(t3 - t2, 4), "gpu_user_vectors_s": round(t4 - t3, 4),
+        "gpu_all_passes_s": round(t5 - t4, 4),
+        "gpu_impressions_per_s": round(n / (t5 - t4), 1),
+        "evaluate_wall_s": round(t_e1 - t_e0, 3),
+        "evaluate_impressions_per_s": round(n / (t_e1 - t_e0), 1),
+        "auc": means[0], "evaluate_equal_to_stagewise": bool(tuple(again) == tuple(means)),
+        "note": "evaluate() = read + plan + all GPU passes (its own clock); gpu_all_passes_s = "
+                "news vectors + user vectors + score_pairs + impression_metrics + nanmean"}
+
+
 def _time_launches(fn, reps, device):
     """Average ms of fn() over reps launches, HIP events on the launch stream."""
     s = torch.cuda.current_stream(device)
@@ -653,6 +705,8 @@ def main():
             leg["max_normwise_rel_err_vs_cpu"] = float(
                 ((yl - ref_cpu).norm(dim=1) / ref_cpu.norm(dim=1).clamp_min(1e-30)).max())
         out["auc_vs_cpu"] = eval_auc_check(model, device)
+    if rank == 0 and world == 1 and not args.no_extras and not args.stream:
+        out["eval_throughput"] = eval_throughput(model, device)
     else:
         out["cpu_baseline"] = None
     for leg in legs.values():

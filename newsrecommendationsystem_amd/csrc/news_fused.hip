@@ -251,29 +251,39 @@ __global__ __launch_bounds__(CLS_T) void classify_titles_kernel(RowMap rm, Title
       if (rm.direct) return (int32_t)(s * FL + i);
       return ((uint64_t)id[i] < (uint64_t)rm.n_rows) ? (int32_t)id[i] : -1;
     };
-    int32_t* cr = tt.crow + s * FL;
-    int c = 0, first_pad = -1;
-    // the rep's row: id 0's (folded) or the first padding token's (per token)
-    auto pad_row = [&](int i) -> int32_t { return rm.direct ? (int32_t)(s * FL + i) : (rm.n_rows > 0 ? 0 : -1); };
+    // the 20 compacted row ids in registers (static indices only: a running
+    // output index spilled the array and turned the stores into 20 scattered
+    // 4-B writes per title), stored as five 16-B writes
+    int32_t out[FL];
+    uint32_t nz = 0;
+#pragma unroll
+    for (int i = 0; i < FL; ++i) nz |= (id[i] != 0 ? 1u : 0u) << i;
+    int c = __popc(nz);
     if (compact) {
+      // the rep's row: id 0's (folded) or the first padding token's (per token)
+      const int first_pad = __ffs(~nz & ((1u << FL) - 1)) - 1;   // (-1: no padding)
+      const int32_t rep_row = rm.direct ? (int32_t)(s * FL + (first_pad < 0 ? 0 : first_pad))
+                                        : (rm.n_rows > 0 ? 0 : -1);
+#pragma unroll
+      for (int q = 0; q < FL; ++q) out[q] = q == c ? rep_row : -2;
 #pragma unroll
       for (int i = 0; i < FL; ++i) {
-        if (id[i] != 0) cr[c++] = row(i);
-        else if (first_pad < 0) first_pad = i;
-      }
+        const int d = __popc(nz & ((1u << i) - 1));   // real token i's compacted position (<= i)
+        const bool real = (nz >> i) & 1;
+        const int32_t r = row(i);
 #pragma unroll
-      for (int q = 0; q < FL; ++q)
-        if (q >= c) cr[q] = q == c ? pad_row(first_pad) : -2;
+        for (int q = 0; q <= i; ++q) out[q] = (real && d == q) ? r : out[q];
+      }
       const int le = c + (c < FL ? 1 : 0);
       bucket = (le + 3) / 4 - 1;
     } else {
 #pragma unroll
-      for (int i = 0; i < FL; ++i) {
-        cr[i] = row(i);
-        c += id[i] != 0;
-      }
+      for (int i = 0; i < FL; ++i) out[i] = row(i);
       bucket = NBK - 1;
     }
+    int4* cr4 = reinterpret_cast<int4*>(tt.crow + s * FL);   // (80-B rows, 16-B aligned: workspace)
+#pragma unroll
+    for (int k = 0; k < FL / 4; ++k) cr4[k] = make_int4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);
     allpad = c == 0;
     tt.cnt[s] = (uint8_t)(compact ? c : FL);
     tt.pad_title[s] = allpad ? 1 : 0;
@@ -1201,7 +1211,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 static size_t fused_news_list_offset() { return (size_t)WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS; }
 static int64_t max_groups(int64_t n_titles) { return (n_titles + FT - 1) / FT + NBK; }
 size_t fused_news_workspace_floats(int64_t n_titles) {
-  return fused_news_list_offset() + NCNT + 4 * (size_t)max_groups(n_titles) + (size_t)NBK * n_titles +
+  return fused_news_list_offset() + NCNT + 4 * (size_t)max_groups(n_titles) + (size_t)NBK * n_titles + 4 +
          (size_t)FL * n_titles + ((size_t)2 * n_titles + 3) / 4;
 }
 namespace {
@@ -1218,7 +1228,8 @@ NewsWs news_ws(float* ws, int64_t n_titles) {
   z.counters = reinterpret_cast<int32_t*>(ws + fused_news_list_offset());
   z.recheck = z.counters + NCNT;
   z.list = z.recheck + 4 * max_groups(n_titles);
-  z.crow = z.list + NBK * n_titles;
+  // (16-B aligned: the classification writes each title's 80-B row as 16-B stores)
+  z.crow = reinterpret_cast<int32_t*>((reinterpret_cast<uintptr_t>(z.list + NBK * n_titles) + 15) & ~uintptr_t(15));
   z.cnt = reinterpret_cast<uint8_t*>(z.crow + FL * n_titles);
   z.pad_title = z.cnt + n_titles;
   return z;

@@ -43,31 +43,81 @@ class NewsCorpus:
         return len(self.ids)
 
 
+def _parse_titles(cells, ids, num_words_title):
+    """The title column's python list literals ("[12, 7, 0, ...]",
+    src/data_preprocess.py:205,239) -> int64 [n, L]: one numpy parse of all
+    cells when every cell is a plain list of L ints, ast.literal_eval per cell
+    otherwise (same values, same errors)."""
+    inner = [c.strip() for c in cells]
+    plain = all(c.startswith("[") and c.endswith("]") and c.count(",") == num_words_title - 1 for c in inner)
+    if plain and inner:
+        body = ",".join(c[1:-1] for c in inner)
+        vals = np.array(body.split(","), dtype=np.int64) if body.strip() else np.zeros(0, np.int64)
+        if vals.size == len(inner) * num_words_title:
+            return vals.reshape(-1, num_words_title)
+    titles = []
+    for nid, c in zip(ids, cells):
+        t = ast.literal_eval(c)
+        if len(t) != num_words_title:
+            raise ValueError(f"title of {nid} has {len(t)} ids, expected {num_words_title}")
+        titles.append(t)
+    return np.array(titles, dtype=np.int64).reshape(-1, num_words_title)
+
+
 def read_news_parsed(path, num_words_title=NUM_WORDS_TITLE):
-    ids, titles = [], []
+    ids, cells = [], []
     with open(path, newline="") as f:
         rd = csv.reader(f, delimiter="\t", quoting=csv.QUOTE_NONE)
         header = next(rd)
         ci, ct = header.index("id"), header.index("title")
         for row in rd:
             ids.append(row[ci])
-            t = ast.literal_eval(row[ct])
-            if len(t) != num_words_title:
-                raise ValueError(f"title of {row[ci]} has {len(t)} ids, expected {num_words_title}")
-            titles.append(t)
-    return NewsCorpus(ids, np.array(titles, dtype=np.int64).reshape(-1, num_words_title))
+            cells.append(row[ct])
+    return NewsCorpus(ids, _parse_titles(cells, ids, num_words_title))
 
 
 class Impression:
-    __slots__ = ("impression_id", "user", "time", "clicked_news", "candidates", "labels")
+    """One behaviors.tsv row. `candidates` / `labels` are parsed from the raw
+    impressions cell ("N1-0 N2-1 ...") on first use (src/evaluate.py:153-157:
+    x.split('-')[0] / int(x.split('-')[1])); EvalPlan parses the cells of a
+    whole split in one pass instead."""
+    __slots__ = ("impression_id", "user", "time", "clicked_news", "raw", "_cands", "_labels")
 
-    def __init__(self, impression_id, user, time, clicked_news, candidates, labels):
+    def __init__(self, impression_id, user, time, clicked_news, candidates=None, labels=None, raw=None):
         self.impression_id = impression_id
         self.user = user
         self.time = time
         self.clicked_news = clicked_news      # the raw history string (user-cache key)
-        self.candidates = candidates          # list of news ids
-        self.labels = labels                  # list of int
+        self.raw = raw                        # the raw impressions cell, or None
+        self._cands = candidates              # list of news ids
+        self._labels = labels                 # list of int
+
+    def _parse(self):
+        toks = [t.split("-") for t in self.raw.split()]
+        self._cands = [t[0] for t in toks]
+        self._labels = [int(t[1]) for t in toks]
+
+    @property
+    def candidates(self):
+        if self._cands is None:
+            self._parse()
+        return self._cands
+
+    @candidates.setter
+    def candidates(self, v):
+        self._cands, self.raw = v, None
+
+    @property
+    def labels(self):
+        if self._labels is None:
+            self._parse()
+        return self._labels
+
+    @labels.setter
+    def labels(self, v):
+        if self._cands is None:
+            self._parse()
+        self._labels, self.raw = v, None
 
 
 def read_behaviors(path):
@@ -82,13 +132,35 @@ def read_behaviors(path):
             cols = line.split("\t")
             cols += [""] * (5 - len(cols))
             hist = cols[3] if cols[3] != "" else " "
-            cands, labels = [], []
-            for tok in cols[4].split():
-                nid, lab = tok.split("-")[0], tok.split("-")[1]
-                cands.append(nid)
-                labels.append(int(lab))
-            out.append(Impression(cols[0], cols[1], cols[2], hist, cands, labels))
+            out.append(Impression(cols[0], cols[1], cols[2], hist, raw=cols[4]))
     return out
+
+
+def parse_impression_cells(impressions):
+    """(candidate ids, labels int32, per-impression counts) of a split, in
+    order. One split of the joined raw cells when every token is `<id>-<label>`
+    with a single '-' (then identical to the per-token split('-') of
+    src/evaluate.py:153-157); the per-impression parse otherwise."""
+    n = len(impressions)
+    raws = [im.raw for im in impressions]
+    if n and all(r is not None for r in raws):
+        joined = " ".join(raws)
+        parts = joined.replace("-", " ").split()
+        counts = np.fromiter((r.count("-") for r in raws), dtype=np.int64, count=n)
+        ntok = int(counts.sum())
+        # every token holds exactly one '-' with text on both sides
+        if len(parts) == 2 * ntok and len(joined.split()) == ntok:
+            labs = parts[1::2]
+            flat = "".join(labs)
+            if len(flat) == ntok and flat.isdigit():   # single-digit labels (MIND's 0/1)
+                labs = np.frombuffer(flat.encode(), dtype=np.uint8).astype(np.int32) - 48
+            else:
+                labs = np.array(labs, dtype=np.int64).astype(np.int32)
+            return parts[0::2], labs, counts
+    names = [c for im in impressions for c in im.candidates]
+    labs = np.fromiter((y for im in impressions for y in im.labels), dtype=np.int64, count=len(names))
+    counts = np.fromiter((len(im.candidates) for im in impressions), dtype=np.int64, count=n)
+    return names, labs.astype(np.int32), counts
 
 
 def history_ids(history_string, num_clicked=NUM_CLICKED):

@@ -24,11 +24,17 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .data import PADDED_NEWS, history_ids, read_behaviors, read_news_parsed
+from .data import PADDED_NEWS, history_ids, parse_impression_cells, read_behaviors, read_news_parsed
 
 
 class EvalPlan:
-    """Host-side index arrays for one split (built once, reused per model)."""
+    """Host-side index arrays for one split (built once, reused per model).
+
+    The impressions cells of the split are parsed in one pass
+    (data.parse_impression_cells) and every candidate / history id is mapped to
+    its corpus row in one flat pass each (the reference looks candidates up
+    inside its per-impression loop, src/evaluate.py:251-255); an unknown id
+    raises KeyError as news2vector[...] does."""
 
     def __init__(self, corpus, impressions, max_count=sys.maxsize, num_clicked=50):
         # the reference breaks when count == max_count before scoring it
@@ -37,26 +43,31 @@ class EvalPlan:
         self.impressions = impressions[:n]
         self.corpus = corpus
         pad = len(corpus)
+        # users keyed by history string, in first-seen order
         hist_of = {}
         hists = []
-        pair_user, cand, labels, offsets = [], [], [], [0]
-        for im in self.impressions:
+        imp_user = np.empty(n, dtype=np.int64)
+        for k, im in enumerate(self.impressions):
             u = hist_of.get(im.clicked_news)
             if u is None:
                 u = hist_of[im.clicked_news] = len(hists)
                 hists.append(im.clicked_news)
-            for c, y in zip(im.candidates, im.labels):
-                cand.append(corpus.index[c])          # KeyError like news2vector[...]
-                labels.append(y)
-                pair_user.append(u)
-            offsets.append(len(cand))
-        self.hist_rows = np.array(
-            [[pad if x == PADDED_NEWS else corpus.index[x] for x in history_ids(h, num_clicked)]
-             for h in hists], dtype=np.int64).reshape(len(hists), num_clicked)
-        self.cand = np.array(cand, dtype=np.int64)
-        self.pair_user = np.array(pair_user, dtype=np.int64)
-        self.labels = np.array(labels, dtype=np.int32)
-        self.offsets = np.array(offsets, dtype=np.int64)
+            imp_user[k] = u
+        cand_names, self.labels, counts = parse_impression_cells(self.impressions)
+        rows_of = corpus.index   # news id -> first row (news2vector[...], evaluate.py:255)
+
+        def lookup(names):
+            return np.fromiter(map(rows_of.__getitem__, names), dtype=np.int64, count=len(names))
+
+        self.cand = lookup(cand_names).astype(np.int64) if cand_names else np.zeros(0, np.int64)
+        self.pair_user = np.repeat(imp_user, counts)
+        self.offsets = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        hist_names = [x for h in hists for x in history_ids(h, num_clicked)]
+        real = np.array([x != PADDED_NEWS for x in hist_names], dtype=bool)
+        rows = np.full(len(hist_names), pad, dtype=np.int64)
+        if real.any():
+            rows[real] = lookup([x for x, r in zip(hist_names, real) if r])
+        self.hist_rows = rows.reshape(len(hists), num_clicked)
         self.num_clicked = num_clicked
 
     @property

@@ -552,6 +552,31 @@ def test_split_gemm_accuracy_matches_f32(device):
         assert e[0] <= 2 * f32[0] + 1e-7 and e[1] <= 2 * f32[1] + 1e-7, errs
 
 
+def test_bench_batch_slice_gemm_arith_vs_fp64(device):
+    """A 128-impression slice of the bench's own config-3 batch (bench.py's
+    model: N(0,1) embedding, V = 70,976; the first 128 impressions of the
+    config-4 stream's rank-0 shard) scored through nrms_forward under each
+    GEMM arithmetic, against the fp64 oracle: f16x3 (the bench default) and
+    x6 within 2x the exact-f32 forward's normwise error (+1e-7)."""
+    import bench
+    from newsrecommendationsystem_amd import _native as N
+    from newsrecommendationsystem_amd import stream as S
+    model = bench.build_model(device)
+    idx = bench.stream_impressions(0, 1, 128, device)
+    cand, clk = S.batch(0, idx, bench.V_WORDS)
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    ref = O.forward(cand.cpu().numpy(), clk.cpu().numpy(), sd, np.float64)
+    errs = {}
+    for name, mode in (("f32", N.NRMS_GEMM_F32), ("x6", N.NRMS_GEMM_SPLIT_BF16X6),
+                       ("f16x3", N.NRMS_GEMM_SPLIT_F16X3)):
+        with N.gemm_arith(mode), torch.no_grad():
+            y = _np(model.forward_ids(cand, clk)).astype(np.float64)
+        errs[name] = float(O.normwise_rel_err(y, ref).max())
+    assert errs["f32"] < 1e-5, errs
+    for name in ("x6", "f16x3"):
+        assert errs[name] <= 2 * errs["f32"] + 1e-7, errs
+
+
 def _attention_pool(qkv, ldq, ids, w, device):
     """nrms_news_attention_pool over a caller-made q|k|v table (one id array)."""
     from newsrecommendationsystem_amd import _native as N
