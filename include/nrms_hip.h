@@ -152,10 +152,9 @@ int32_t nrms_last_hip_error(void);
 int32_t nrms_embedding_gather(const int64_t* ids, int64_t n_tok, const float* table,
                               int64_t V, int32_t D, float* out, hipStream_t stream);
 
-/* Row stride (floats) of the q|k|v rows the fused kernels prefer: 3D rounded
- * up to whole 128-B lines (928 for D = 300). Rows at this stride are written
- * by the projection GEMM without partial cache lines (3,600-B rows wrote
- * 1.27x their bytes); any stride >= 3D that is a multiple of 4 is accepted. */
+/* Row stride (floats) of the q|k|v rows the fused kernels prefer: 3D (900 for
+ * D = 300; rows padded to whole 128-B lines, 928, measured 5 % slower per
+ * step: DESIGN.md). Any stride >= 3D that is a multiple of 4 is accepted. */
 int32_t nrms_qkv_row_stride(int32_t D);
 
 /* Q|K|V projection (multihead_self.py:53-58): qkv[m * ld_qkv + 0:3D] =

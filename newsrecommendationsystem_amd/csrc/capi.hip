@@ -80,8 +80,7 @@ WeightRows qkv_rows(const nrms_encoder_weights_t* w) {
   return r;
 }
 
-// q|k|v row stride of the hot path: padded to whole 128-B lines when the fused
-// kernels take the shape, 3D (the stage kernels' layout) otherwise
+// q|k|v row stride of the hot path (nrms_qkv_row_stride; 3D since round 3)
 int64_t news_ld(const nrms_encoder_weights_t* w, int32_t L) {
   return fused_news_supported(L, w->d_model, w->n_heads, w->query_dim) ? qkv_row_stride(w->d_model)
                                                                          : 3 * (int64_t)w->d_model;
@@ -151,7 +150,7 @@ int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int
                              prepacked, direct_rows, -1, classified);
   if (direct_rows) ids_a = ids_b = nullptr;   // per-token rows: the ids only classify (fused kernel)
   // stage kernels: any row stride >= 3D (packed rows, or the folded table's
-  // padded 128-B-line rows that nrms_qkv_row_stride reports)
+  // rows of nrms_qkv_row_stride)
   int32_t st = launch_mhsa(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, L, w->n_heads, kDK, ctx, s);
   if (st) return st;
   st = launch_gemm_additive_score(ctx, n_seq * L, D, w->w_add, w->b_add, w->q_add, w->query_dim,

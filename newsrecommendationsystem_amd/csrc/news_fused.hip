@@ -55,7 +55,7 @@ constexpr int FNT = 13;              // N tiles of 16 (208 >= Q)
 constexpr int SC = 328;              // context row stride in floats (== 8 mod 32)
 constexpr int NTHR = 256;
 constexpr int WAP_FLOATS = FKG * FNT * 64 * 4;             // packed Wa
-constexpr int ROW = 3 * FD;                                // q|k|v row: [q 300 | k 300 | v 300]
+constexpr int ROW = (3 * FD + 31) / 32 * 32;               // zero / NaN row slots (928 floats: room for any q|k|v offset)
 constexpr int SPECIAL_FLOATS = 2 * ROW;                    // zero row + NaN row
 // after the context tile: row partials [80][PART_STRIDE] (the four waves' N-tile
 // sums + the N-tile-12 sum), row pointers [2][80] (u64), title meta [2][8] and
@@ -413,12 +413,23 @@ struct TitleSet {
 // Float offsets, within one q|k|v row, of what lane (head slot hl, x) of wave
 // (head group) g loads: q / k dims 4c..4c+3 of head h = 4g + hl, and v dims
 // 5x..5x+3 and 5x+4.
+#ifdef NRMS_QKV_PERM
+// (probe) chunk-major q / k sections: chunk c of the 4 heads of group g contiguous
+struct QkvOffsets {
+  __device__ static int qk(int g, int hl, int c) { return g < 3 ? 80 * g + 16 * c + 4 * hl : 240 + 12 * c + 4 * hl; }
+  __device__ static int q(int g, int hl, int c) { return qk(g, hl, c); }
+  __device__ static int k(int g, int hl, int c) { return 304 + qk(g, hl, c); }
+  __device__ static int v4(int g, int hl, int x) { return 608 + FDK * (4 * g + hl) + 5 * x; }
+  __device__ static int v1(int g, int hl, int x) { return 608 + FDK * (4 * g + hl) + 5 * x + 4; }
+};
+#else
 struct QkvOffsets {
   __device__ static int q(int g, int hl, int c) { return FDK * (4 * g + hl) + 4 * c; }
   __device__ static int k(int g, int hl, int c) { return FD + FDK * (4 * g + hl) + 4 * c; }
   __device__ static int v4(int g, int hl, int x) { return 2 * FD + FDK * (4 * g + hl) + 5 * x; }
   __device__ static int v1(int g, int hl, int x) { return 2 * FD + FDK * (4 * g + hl) + 5 * x + 4; }
 };
+#endif
 
 // 4 floats from a 4-byte-aligned address (V slices start at 5x floats).
 typedef float float4_a4 __attribute__((ext_vector_type(4), aligned(4)));
@@ -1270,7 +1281,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   if (classified) *classified = false;
   if (n_titles == 0) return NRMS_OK;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)ws) % 16) return NRMS_ERR_UNSUPPORTED;
-  if (ldq < ROW || ldq % 4) return NRMS_ERR_UNSUPPORTED;   // float4 q / k slices
+  if (ldq < 3 * FD || ldq % 4) return NRMS_ERR_UNSUPPORTED;   // float4 q / k slices
   if (max_groups(n_titles) >= (1ll << 27)) return NRMS_ERR_UNSUPPORTED;   // recheck entries: group << 4 | mask
   // F16X3: f16x3 main pass, x6 recheck pass
   const int arith = gemm_arith();

@@ -130,11 +130,12 @@ struct WeightRows {
 };
 
 // Row stride (floats) of the q|k|v rows the hot path writes and the fused
-// kernels read: 3D rounded up to 32 floats = whole 128-B lines (928 for
-// D = 300), so no cache line is shared by two GEMM column tiles or two rows
-// (the unpadded 3,600-B rows wrote 1.27x the algorithmic bytes: partial
-// lines at every tile boundary).
-inline int64_t qkv_row_stride(int D) { return ((int64_t)3 * D + 31) / 32 * 32; }
+// kernels read: 3D, unpadded. Rows padded to whole 128-B lines (928 for
+// D = 300) were measured slower end to end (0.911 vs 0.869 ms per bench step,
+// same box, 2 reps each; 912 / 960: 0.877 / 0.906): the fused kernels' gathers
+// read the same 16-B slice offset from every row, and with every row on a
+// line boundary those slices all fall at one offset within the line.
+inline int64_t qkv_row_stride(int D) { return (int64_t)3 * D; }
 
 // Process-wide GEMM arithmetic (nrms_set_gemm_arith; defined in capi.hip).
 int gemm_arith();

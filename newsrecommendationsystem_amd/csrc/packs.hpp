@@ -14,7 +14,7 @@ constexpr int D = 300, Q = 200;
 constexpr int KS = 10;                          // bf16 / f16 k-steps of 32 (K 300 -> 320)
 constexpr int NT = 13;                          // N tiles of 16 (208 >= Q)
 constexpr int KG = 19;                          // f32 k-groups of 16 (K 300 -> 304)
-constexpr int ROW = 3 * D;                      // q|k|v row
+constexpr int ROW = (3 * D + 31) / 32 * 32;     // q|k|v row slot of the zero / NaN rows (qkv_row_stride)
 // news: [x6 planes | f32 fragments] (max), zero + NaN q|k|v rows, f16 planes
 constexpr int NEWS_WAP_F32 = KG * NT * 64 * 4;
 constexpr int NEWS_WAP_X6 = KS * NT * 3 * 64 * 4;

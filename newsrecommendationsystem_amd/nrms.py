@@ -135,7 +135,7 @@ class NewsEncoder(nn.Module):
         tab = self.table()
         V, D = tab.shape
         w, keep = self.weights()
-        ld = N.load().nrms_qkv_row_stride(D)   # rows padded to whole 128-B lines
+        ld = N.load().nrms_qkv_row_stride(D)
         qkv = torch.empty(V, ld, dtype=torch.float32, device=tab.device)
         nb = N.load().nrms_qkv_project_workspace_size(D)   # the pre-split-W projection, as nrms_forward's
         ws = torch.empty(nb, dtype=torch.uint8, device=tab.device)

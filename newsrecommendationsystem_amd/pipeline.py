@@ -43,7 +43,7 @@ class ForwardPlan:
         D = self.D
         qkv_rows = self.V if self.folded else n_all * L
         lib = N.load()
-        # the fused tails read rows padded to whole 128-B lines; the stage kernels packed rows
+        # rows of nrms_qkv_row_stride for the fused tails, packed 3D rows for the stage kernels
         self.ldq = lib.nrms_qkv_row_stride(D) if fused else 3 * D
         self.uldq = lib.nrms_qkv_row_stride(D) if fused and n_clicked <= 64 else 3 * D
         self.qkv = torch.empty(qkv_rows, self.ldq, **f32)

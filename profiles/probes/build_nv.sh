@@ -5,8 +5,9 @@
 set -euo pipefail
 cd "$(dirname "$0")"
 NAME=$1; shift
-CXX=(/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -I ../../include "$@"
-     -mllvm -amdgpu-sched-strategy=iterative-ilp news_variants.hip)
+# (the product build uses the default scheduler for news_fused.hip; pass
+# -mllvm -amdgpu-sched-strategy=... to try another)
+CXX=(/opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -I ../../include "$@" news_variants.hip)
 "${CXX[@]}" -o "nv_${NAME}" &
 "${CXX[@]}" -DNRMS_NO_STAMPS -o "nv_${NAME}_ns" &
 wait

@@ -244,8 +244,8 @@ def test_news_encoder_title_lengths_vs_oracle(device, L):
 
 @pytest.mark.parametrize("L", [5, 20, 32, 50])
 def test_news_encoder_cached_folded_table_title_lengths(device, L):
-    """The eval path with the default cached folded table (padded 128-B-line
-    rows, nrms_qkv_row_stride) at title lengths the fused kernel does not take:
+    """The eval path with the default cached folded table (rows of
+    nrms_qkv_row_stride) at title lengths the fused kernel does not take:
     the stage kernels read the padded rows (L != 20 used to fail)."""
     V = 512
     sd = W.nrms_state(7, V)
@@ -303,9 +303,9 @@ def test_fused_news_tail_vs_stages(device, n, gemm_mode):
     sd = W.nrms_state(21, V)
     m = _module(sd, V, device, hip_cache_folded_table=False)
     ne = m.news_encoder
-    qkv = ne.folded_table()                     # rows padded to nrms_qkv_row_stride
+    qkv = ne.folded_table()                     # rows of nrms_qkv_row_stride
     packed = qkv[:, :900].contiguous()          # the stage kernels' packed layout
-    assert qkv.shape[1] == N.load().nrms_qkv_row_stride(300) == 928
+    assert qkv.shape[1] == N.load().nrms_qkv_row_stride(300) == 900
     ids = torch.from_numpy(W.titles(21, 40 + n, n, V, min_len=1)).to(device)
     na = n // 2
     # a NULL first id array means "identity rows" in the ABI, so never pass an empty one
