@@ -7,7 +7,8 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 PKG=$ROOT/newsrecommendationsystem_amd
 OBJ=$PKG/_build
 TMP=$ROOT/_ab/obj_$NAME; mkdir -p "$TMP"
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I "$ROOT/include" -I "$PKG/csrc" "$@" -c "$PKG/csrc/$SRC" -o "$TMP/${SRC%.hip}.o"
+# (SRC_FILE=path: compile that file in place of csrc/<source.hip>)
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -I "$ROOT/include" -I "$PKG/csrc" "$@" -c "${SRC_FILE:-$PKG/csrc/$SRC}" -o "$TMP/${SRC%.hip}.o"
 objs=()
 for o in "$OBJ"/*.o; do
   b=$(basename "$o"); [ "$b" = "${SRC%.hip}.o" ] && objs+=("$TMP/$b") || objs+=("$o")

@@ -228,10 +228,10 @@ struct Titles {
 // of its compacted length, except (dedupe) the all-padding titles: those are
 // one vector, encoded once for the lowest of them (rep, appended to its
 // bucket by the main pass) and copied. One atomicAdd per bucket and one
-// atomicMin per 1,024-title block (device-scope atomics on one address
+// atomicMin per 256-title block (device-scope atomics on one address
 // serialise). List order is arbitrary: a title's result does not depend on the
 // group or slot it is encoded in.
-constexpr int CLS_T = 1024, CLS_W = CLS_T / 64;
+constexpr int CLS_T = 256, CLS_W = CLS_T / 64;   // (1,024-thread blocks: 55 blocks at config 3, 1.7x slower)
 __global__ __launch_bounds__(CLS_T) void classify_titles_kernel(RowMap rm, Titles tt, int dedupe, int compact) {
   __shared__ int wcnt[NBK][CLS_W], wbase[NBK][CLS_W], wrep[CLS_W];
   const int64_t s = (int64_t)blockIdx.x * CLS_T + threadIdx.x;
@@ -502,6 +502,10 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   constexpr bool X6 = MODE == 1;
   constexpr bool H3 = MODE == 2;
   static_assert(!(H3 && EXACT), "the F16X3 main pass is rechecked by the x6 kernel");
+  if constexpr (EXACT) {
+    // nothing flagged (every real input): leave before the prologue
+    if (__builtin_amdgcn_readfirstlane(*rl.count) == 0) return;
+  }
   if constexpr (!EXACT) {
     if (ur.list)   // (workgroup-uniform; the padding classification ran in an earlier launch)
       for (int64_t m0 = (int64_t)blockIdx.x * URL_ROWS; m0 < ur.n_rows; m0 += (int64_t)gridDim.x * URL_ROWS) {
