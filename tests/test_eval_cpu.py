@@ -85,3 +85,46 @@ def test_planted_teacher_gives_informative_auc(tmp_path):
                                       temperature=0.5)
     means, _, _ = EO.evaluate(sd, corpus, imps)
     assert means[0] > 0.6   # the teacher's own scores rank its labels well
+
+
+def _raw(cell):
+    return Dt.Impression("1", "U1", "t", " ", raw=cell)
+
+
+@pytest.mark.parametrize("cells", [
+    ["N1-0 N2-1", "N3-1"],                 # the MIND form: one pass over the joined cells
+    ["N1-10 N2-1", "N3-0"],                # multi-digit label: the int parse
+    ["N-1-0 N2-1"],                        # an id holding '-': per-token split('-'), as the reference
+    ["N1-0  N2-1 ", " N3-1"],              # ragged whitespace
+])
+def test_impression_cell_parse_matches_per_token_split(cells):
+    """parse_impression_cells == the reference's per-token x.split('-')[0] /
+    int(x.split('-')[1]) (src/evaluate.py:153-157) on every cell form."""
+    imps = [_raw(c) for c in cells]
+    names, labels, counts = Dt.parse_impression_cells(imps)
+    want_n = [t.split("-")[0] for c in cells for t in c.split()]
+    want_l = [int(t.split("-")[1]) for c in cells for t in c.split()]
+    assert names == want_n and labels.tolist() == want_l and labels.dtype == np.int32
+    assert counts.tolist() == [len(c.split()) for c in cells]
+    # the lazily parsed per-impression view agrees
+    assert [c for im in imps for c in im.candidates] == want_n
+    assert [y for im in imps for y in im.labels] == want_l
+
+
+def test_impression_cell_without_label_raises():
+    # a token with no '-<label>' (MIND's test split) fails as in the reference
+    with pytest.raises(IndexError):
+        Dt.parse_impression_cells([_raw("N1 N2-1")])
+
+
+def test_title_cells_parse_matches_literal_eval():
+    """read_news_parsed's one-pass title parse == ast.literal_eval per cell,
+    including the fallback for a cell that is not a plain list of L ints."""
+    import ast
+    cells = ["[1, 2, 0]", "[7,8,9]", "[0, 0, 0]"]
+    got = Dt._parse_titles(cells, ["a", "b", "c"], 3)
+    assert got.tolist() == [ast.literal_eval(c) for c in cells]
+    odd = ["[1, 2, 3]", "(4, 5, 6)"]                          # a tuple literal: per-cell path
+    assert Dt._parse_titles(odd, ["a", "b"], 3).tolist() == [[1, 2, 3], [4, 5, 6]]
+    with pytest.raises(ValueError):
+        Dt._parse_titles(["[1, 2]"], ["a"], 3)
