@@ -1349,7 +1349,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
                      b_add, q_add, out, rl, ur NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
   // the recheck pass: reads the count the main pass left; exits at once when 0
-  const int64_t blocks_x = blocks < 64 ? blocks : 64;
+  const int64_t blocks_x = blocks < 16 ? blocks : 16;   // (flagged groups are rare; a smaller grid launches faster)
   hipLaunchKernelGGL(kern_exact, dim3((unsigned)blocks_x), dim3(NTHR), lds_bytes_exact, s, qkv, ldq, rm, ts,
                      ws, b_add, q_add, out, rl, UserRows{nullptr, 0, nullptr, nullptr, nullptr} NRMS_TIMING_ARG);
   if (int32_t st = launch_status()) return st;
