@@ -38,6 +38,8 @@
 #include "nrms_common.hpp"
 #include "packs.hpp"
 
+#include <type_traits>
+
 namespace nrms {
 namespace {
 
@@ -157,6 +159,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     L = L_all - npad + (npad > 0 ? 1 : 0);
     m0 = npad > 1 ? npad : 1;
   }
+  L = __builtin_amdgcn_readfirstlane(L);   // (workgroup-uniform: scalar loop bounds below)
   auto row = [&](int i) -> const float* {
     if (compact) return qkv + (int64_t)urow[i] * ldq;
     int64_t m = s * L + i;
@@ -201,13 +204,9 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   if (has) {
     // exp(d / sqrt(d_k)) as v_exp_f32(d · log2(e) / sqrt(d_k)), as the news kernel
     const float rs = 1.4426950408889634f / sqrtf((float)UDK);
-    // Keys j >= L read row L-1 and get weight 0 (no per-key branch, so the
-    // independent dot products interleave); adding 0 changes no sum.
     const float sqrt_dk = sqrtf((float)UDK);
-    bool exact = false;   // the row's weights take the reference's exp (kExpRecheck)
-    auto dot = [&](int j) {
-      const int jj = j < L ? j : L - 1;
-      const float4* kr = reinterpret_cast<const float4*>(tile + jj * URS + UDK * h);
+    auto dot = [&](int j) __attribute__((always_inline)) {
+      const float4* kr = reinterpret_cast<const float4*>(tile + j * URS + UDK * h);
       float d = 0.f;
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
@@ -219,47 +218,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       }
       return d;
     };
-    auto raw = [&](int j) { return j < L ? __builtin_amdgcn_exp2f(dot(j) * rs) : 0.f; };
-    auto raw_exact = [&](int j) { return j < L ? ref_exp(dot(j), sqrt_dk) : 0.f; };
-    // LMAX = 64 would not fit the exps in registers at 16 waves: recompute
-    // them in the second pass (expf is deterministic: same weights).
-    constexpr bool kKeep = LMAX <= 50;
-    float e[kKeep ? LMAX : 1];
-    constexpr int kUnroll = kKeep ? LMAX : 4;
-    float sum = 0.f;
-#pragma unroll kUnroll
-    for (int j = 0; j < LMAX; ++j) {
-      const float x = raw(j);
-      if constexpr (kKeep) e[j] = x;
-      if (j == 0)
-        for (int c = 0; c < m0; ++c) sum += x;   // (row 0's multiplicity, one addition at a time)
-      else
-        sum += x;
-    }
-    if (exp_row_needs_recheck(sum)) {   // rare: rows near fp32 overflow
-      exact = true;
-      sum = 0.f;
-#pragma unroll kUnroll
-      for (int j = 0; j < LMAX; ++j) {
-        const float x = raw_exact(j);
-        if constexpr (kKeep) e[j] = x;
-        if (j == 0)
-          for (int c = 0; c < m0; ++c) sum += x;
-        else
-          sum += x;
-      }
-    }
-    const float inv = 1.0f / (sum + 1e-8f);
-#pragma unroll
-    for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
-#pragma unroll kUnroll
-    for (int j = 0; j < LMAX; ++j) {
-      const int jj = j < L ? j : L - 1;
-      float ej;
-      if constexpr (kKeep) ej = e[j]; else ej = exact ? raw_exact(j) : raw(j);
-      float a = ej * inv;
-      if (j == 0 && m0 > 1) a *= (float)m0;
-      const float4* vr = reinterpret_cast<const float4*>(tile + jj * URS + UD + UDK * h);
+    auto axpy = [&](float a, int j) __attribute__((always_inline)) {
+      const float4* vr = reinterpret_cast<const float4*>(tile + j * URS + UD + UDK * h);
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
         const float4 v4 = vr[t];
@@ -267,6 +227,64 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         acc[4 * t + 1] = fmaf(a, v4.y, acc[4 * t + 1]);
         acc[4 * t + 2] = fmaf(a, v4.z, acc[4 * t + 2]);
         acc[4 * t + 3] = fmaf(a, v4.w, acc[4 * t + 3]);
+      }
+    };
+#pragma unroll
+    for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
+    // Fast path, one pass over the user's L keys (a rolled loop, four keys per
+    // iteration: their dot products interleave; keys past L in the last
+    // iteration read row L-1 with weight 0): sum = the raw exps in the
+    // reference's key order (row 0 counted m0 times, one addition at a time),
+    // acc = sum_j e_j v_j, ctx = acc / (sum + 1e-8). Only the normalisation
+    // moves (after the sum instead of per weight: fp32 rounding). No exp is
+    // kept, so the work is ~L, not LMAX, keys per query.
+    float sum = 0.f;
+    for (int j0 = 0; j0 < L; j0 += 4) {
+      float e[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int j = j0 + u;
+        e[u] = j < L ? __builtin_amdgcn_exp2f(dot(j < L ? j : L - 1) * rs) : 0.f;
+      }
+      if (j0 == 0) {
+        for (int c = 0; c < m0; ++c) sum += e[0];   // (row 0's multiplicity)
+        e[0] *= (float)m0;
+      } else {
+        sum += e[0];
+      }
+      sum += e[1];
+      sum += e[2];
+      sum += e[3];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) axpy(e[u], j0 + u < L ? j0 + u : L - 1);
+    }
+    bool finite = true;
+#pragma unroll
+    for (int t = 0; t < UDK; ++t) finite &= __builtin_isfinite(acc[t]);
+    if (!exp_row_needs_recheck(sum) && finite) {
+      const float inv = 1.0f / (sum + 1e-8f);
+#pragma unroll
+      for (int t = 0; t < UDK; ++t) acc[t] *= inv;
+    } else {
+      // rare (rows near fp32 overflow, non-finite inputs, or a context past
+      // fp32 before the normalisation): the reference's own arithmetic and
+      // order -- ref_exp weights, e_j / (sum + 1e-8) per key, then sum_j P_j v_j
+      // (kExpRecheck); the exps are recomputed in the second pass
+      sum = 0.f;
+      for (int j = 0; j < L; ++j) {
+        const float x = ref_exp(dot(j), sqrt_dk);
+        if (j == 0)
+          for (int c = 0; c < m0; ++c) sum += x;
+        else
+          sum += x;
+      }
+      const float inv = 1.0f / (sum + 1e-8f);
+#pragma unroll
+      for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
+      for (int j = 0; j < L; ++j) {
+        float a = ref_exp(dot(j), sqrt_dk) * inv;
+        if (j == 0 && m0 > 1) a *= (float)m0;
+        axpy(a, j);
       }
     }
     if constexpr (MODE == 2) {
@@ -344,7 +362,10 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   NRMS_U_STAMP(2)   // context split + stores
 
   // ---------------- 2. additive GEMM + tanh·q row partials ----------------
-  if (w < UNT) {
+  // M-tiles past row L - 1 are skipped: one copy of the GEMM per live M-tile
+  // count MTE = ceil(L / 16) (rows L.. of the last tile read row L - 1 and are dropped)
+  auto gemm = [&](auto mtc) {
+    constexpr int MT = decltype(mtc)::value;
     const int lm = lane & 15, kq = lane >> 4;
     float qv[NTPW], bv[NTPW];
     [[maybe_unused]] int ewv[NTPW];   // MODE 2: column exponents
@@ -463,6 +484,13 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         }
       }
     }
+  };
+  if (w < UNT) {
+    const int mte = (L + 15) / 16;
+    if (mte <= 1) gemm(std::integral_constant<int, 1>{});
+    else if (mte == 2) gemm(std::integral_constant<int, 2 < MT ? 2 : MT>{});
+    else if (mte == 3) gemm(std::integral_constant<int, 3 < MT ? 3 : MT>{});
+    else gemm(std::integral_constant<int, MT>{});
   }
   __syncthreads();
   NRMS_U_STAMP(3)   // additive GEMM + tanh·q
