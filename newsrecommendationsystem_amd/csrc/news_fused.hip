@@ -456,15 +456,6 @@ __device__ __forceinline__ const NRMS_GLOBAL T* gptr(const float* p) {
 #define NRMS_STAMP(k)
 #endif
 
-// tanh(x) = 1 - 2 / (e^2x + 1): v_exp_f32 + v_rcp_f32, absolute error ~1e-7
-// over the whole range (the additive scores are sums of q_n tanh(.) with
-// |q_n| <= 0.1, so absolute error is what matters); saturates to +-1 and
-// propagates NaN.
-__device__ __forceinline__ float tanh_fast(float x) {
-  const float e = __builtin_amdgcn_exp2f(2.8853900817779268f * x);   // e^(2x)
-  return fmaf(-2.0f, __builtin_amdgcn_rcpf(e + 1.0f), 1.0f);
-}
-
 // Sum over the 16 lanes of a DPP row (all 16 get the total): quad butterflies,
 // then half-row and row mirrors. VALU only, no LDS crossbar round trips.
 __device__ __forceinline__ float row16_sum(float v) {
@@ -473,6 +464,16 @@ __device__ __forceinline__ float row16_sum(float v) {
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false)); // row_half_mirror
   v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false)); // row_mirror
   return v;
+}
+
+// Four independent DPP row sums, stage by stage: each stage's four adds fill
+// the DPP read-after-write wait states the single-value form pads with s_nop.
+__device__ __forceinline__ void row16_sum4(float (&v)[4]) {
+#define NRMS_DPP4(CTRL)                                                                                   \
+  _Pragma("unroll") for (int r = 0; r < 4; ++r) v[r] += __builtin_bit_cast(                              \
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v[r]), CTRL, 0xF, 0xF, false));
+  NRMS_DPP4(0xB1) NRMS_DPP4(0x4E) NRMS_DPP4(0x141) NRMS_DPP4(0x140)
+#undef NRMS_DPP4
 }
 
 // value of lane ^ 1 / lane ^ 2 within the quad (DPP quad_perm)
@@ -656,6 +657,26 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   const int colx = 192 + lm;
   const bool xok = colx < FQ;
   const float qx = xok ? q_add[colx] : 0.f, bx = xok ? b_add[colx] : 0.f;
+  // B epilogue: q tanh(y + b) = q - 2q / (e^(2(y + b)) + 1), so a lane's
+  // partial over its N-tiles starts at sum_j q_j and adds -2 q_j r_j with
+  // r_j = rcp(exp2(fma(acc, 2 log2(e) s, 2 log2(e) b_j)) + 1); s = 2^-11 undoes
+  // the split-f16 accumulator scaling (exact) -- five VALU per element
+  // (v_exp_f32 + v_rcp_f32: absolute error ~1e-7 over the whole range -- the
+  // scores are sums of q_n tanh(.) with |q_n| <= 0.1, so absolute error is what
+  // matters; saturates to +-1 and propagates NaN)
+  constexpr float kC2 = 2.8853900817779268f;   // 2 log2(e)
+  const float ysc = H3 ? kC2 * kLoUnscale : kC2;
+  float cbv[3], m2q[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    cbv[j] = kC2 * bv[j];
+    m2q[j] = -2.0f * qv[j];
+  }
+  const float qsum = (qv[0] + qv[1]) + qv[2];
+  const float cbx = kC2 * bx, m2qx = -2.0f * qx;
+  auto tq = [&](float a, float cb) __attribute__((always_inline)) {
+    return __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(fmaf(a, ysc, cb)) + 1.0f);
+  };
   const float4* Bp = reinterpret_cast<const float4*>(WaP) + lane;
   const float* Aw = ctxL + lm * SC + 4 * kq;
 
@@ -1022,12 +1043,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
             kstep(ks + 1, b1);
             __builtin_amdgcn_sched_barrier(0);
           }
-#pragma unroll
-          for (int mt = 0; mt < NB; ++mt)
-#pragma unroll
-            for (int j = 0; j < 3; ++j) acc[mt][j] *= kLoUnscale;
-          accX *= kLoUnscale;
-          accX2 *= kLoUnscale;
+          // (the 2^-11 unscale is folded into the epilogue's exp argument)
         } else {
           float4 bb[4], bn4[4];
 #pragma unroll
@@ -1063,33 +1079,45 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         // tanh blocks (pinned by sched_barrier): issued all at once ahead of the
         // tanh work, the in-order issue stalls the VALU behind the gather's
         // address/TA queue.
+        // Main pass: the next group is of this bucket or a smaller one (buckets
+        // run NB = 5 .. 1), so its slices are tokens < 4 NB: loaded
+        // unconditionally (slots past its rows, or no next group, read the zero
+        // row), no zero fill. The recheck pass walks groups of any bucket.
 #pragma unroll
         for (int mt = 0; mt < NB; ++mt) {
-          if (mt < nb_next) prefetch_qk_tok(nbuf, mt);
+          if (!EXACT || mt < nb_next) prefetch_qk_tok(nbuf, mt);
           else zero_qk_tok(mt);
           __builtin_amdgcn_sched_barrier(0);
+          float p[4];
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            float p = 0.f;
+            p[r] = qsum;
 #pragma unroll
-            for (int j = 0; j < 3; ++j) p = fmaf(qv[j], tanh_fast(acc[mt][j][r] + bv[j]), p);
-            p = row16_sum(p);
-            const int row = 16 * mt + 4 * kq + r;
-            if (lm == 0) part[PART_STRIDE * row + w] = p;
-            const bool own_x = (mt == w && w < NB) || (NB == 5 && w == 0 && mt == 4);
-            if (own_x) {
-              const float ax = (NB == 5 && mt == 4) ? accX2[r] : accX[r];
-              float px = fmaf(qx, tanh_fast(ax + bx), 0.f);
-              px = row16_sum(px);
-              if (lm == 0) part[PART_STRIDE * row + 4] = px;
-            }
+            for (int j = 0; j < 3; ++j) p[r] = fmaf(m2q[j], tq(acc[mt][j][r], cbv[j]), p[r]);
+          }
+          row16_sum4(p);
+          if (lm == 0)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) part[PART_STRIDE * (16 * mt + 4 * kq + r) + w] = p[r];
+          const bool own_x = (mt == w && w < NB) || (NB == 5 && w == 0 && mt == 4);
+          if (own_x) {
+            float px[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              px[r] = fmaf(m2qx, tq((NB == 5 && mt == 4) ? accX2[r] : accX[r], cbx), qx);
+            row16_sum4(px);
+            if (lm == 0)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) part[PART_STRIDE * (16 * mt + 4 * kq + r) + 4] = px[r];
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (EXACT) {
 #pragma unroll
-        for (int j = NB; j < 5; ++j) {
-          if (j < nb_next) prefetch_qk_tok(nbuf, j);
-          else zero_qk_tok(j);
+          for (int j = NB; j < 5; ++j) {
+            if (j < nb_next) prefetch_qk_tok(nbuf, j);
+            else zero_qk_tok(j);
+          }
         }
       }
       NRMS_STAMP(4)
@@ -1131,17 +1159,20 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         for (int i = 0; i < NB; ++i) mx = mult[i] > 0.f ? nan_max(mx, sc[i]) : mx;
         mx = nan_max(mx, quad_xor1(mx));
         mx = nan_max(mx, quad_xor2(mx));
+        // exp on v_exp_f32 (arguments <= 0: no overflow; NaN propagates) and one
+        // reciprocal per title instead of a division per row (fp32 rounding)
         float ex[NB], sum = 0.f;
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
-          ex[i] = mult[i] > 0.f ? expf(sc[i] - mx) * mult[i] : 0.f;
+          ex[i] = mult[i] > 0.f ? __builtin_amdgcn_exp2f((sc[i] - mx) * 1.4426950408889634f) * mult[i] : 0.f;
           sum += ex[i];
         }
         sum += quad_xor1(sum);
         sum += quad_xor2(sum);
+        const float rsum = __builtin_amdgcn_rcpf(sum);
         float wt[NB];
 #pragma unroll
-        for (int i = 0; i < NB; ++i) wt[i] = ex[i] / sum;
+        for (int i = 0; i < NB; ++i) wt[i] = ex[i] * rsum;
         // pz[m][r'] = dim 5r' + m of head h, summed over this lane's rows, then
         // the quad; unused slots (last row block only) are skipped, not
         // weighted by 0 (their context may be non-finite)
@@ -1174,7 +1205,12 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         // V slices of the next group: issued here, after O is dead (holding both
         // through the B epilogue spills); the S^T phase of the next group covers
         // most of their latency
-        prefetch_v(nbuf, nb_next);
+        if constexpr (EXACT) {
+          prefetch_v(nbuf, nb_next);
+        } else {
+#pragma unroll
+          for (int kk = 0; kk < LR; ++kk) prefetch_v_tok(nbuf, kk);   // (as the Q|K slices above)
+        }
       }
       NRMS_STAMP(6)
     }
