@@ -16,9 +16,10 @@
  *     memory and never synchronises the stream; any host thread may call it
  *     on any stream, and every call is capturable into a hipGraph. It keeps
  *     no per-call state. Process-wide state is limited to: the GEMM
- *     arithmetic (nrms_set_gemm_arith, an atomic read at enqueue time), the
- *     last HIP error (thread-local), and a mutex-guarded record of which
- *     (device, kernel) pairs have had their dynamic-LDS limit raised.
+ *     arithmetic, title-dedupe and token-compaction switches (atomics read at
+ *     enqueue time; each can be overridden per host thread), the last HIP
+ *     error (thread-local), and a mutex-guarded record of which (device,
+ *     kernel) pairs have had their dynamic-LDS limit raised.
  *   - fp32 row-major everywhere; ids are int64 (the reference's LongTensor).
  *   - Every function returns NRMS_OK (0) or an nrms_status_t error code; a
  *     launch failure returns NRMS_ERR_HIP and the HIP error is kept for
@@ -50,7 +51,9 @@ extern "C" {
  *    Q|K|V weight (their *_workspace_size functions grew). */
 /* 5: nrms_set_token_compaction; title-level padding dedupe; the encode /
  *    forward workspaces hold the title buckets (*_workspace_size grew). */
-#define NRMS_ABI_VERSION 5
+/* 6: nrms_set_thread_gemm_arith / _title_dedupe / _token_compaction
+ *    (per-thread overrides of the process-wide switches). */
+#define NRMS_ABI_VERSION 6
 
 typedef enum {
   NRMS_OK = 0,
@@ -142,6 +145,17 @@ int32_t nrms_set_title_dedupe(int32_t on);
  * time; returns the previous setting. NRMS_COMPACT=0 in the environment
  * starts with it off. */
 int32_t nrms_set_token_compaction(int32_t on);
+
+/* Per-thread overrides of the three process-wide switches above (ABI 6): a
+ * value >= 0 applies to the work the CALLING host thread enqueues, in place
+ * of the process-wide setting, so host threads driving different arithmetics
+ * (or dedupe / compaction settings) on different streams do not race; -1
+ * clears the thread's override. Each returns the thread's previous override
+ * (-1: none), or -NRMS_ERR_INVALID_ARG. nrms_get_gemm_arith reports the
+ * calling thread's effective mode. */
+int32_t nrms_set_thread_gemm_arith(int32_t mode);
+int32_t nrms_set_thread_title_dedupe(int32_t on);
+int32_t nrms_set_thread_token_compaction(int32_t on);
 
 int32_t nrms_abi_version(void);
 const char* nrms_status_string(int32_t status);

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NRMS_LIB_PATH") or os.path.join(_PKG, "libnrms_hip.so")   # override: A/B builds
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
 NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32, NRMS_GEMM_SPLIT_F16X3 = 0, 1, 2
@@ -41,6 +41,9 @@ SIGNATURES = {
     "nrms_set_gemm_arith": (_i32, [_i32]),
     "nrms_set_title_dedupe": (_i32, [_i32]),
     "nrms_set_token_compaction": (_i32, [_i32]),
+    "nrms_set_thread_gemm_arith": (_i32, [_i32]),
+    "nrms_set_thread_title_dedupe": (_i32, [_i32]),
+    "nrms_set_thread_token_compaction": (_i32, [_i32]),
     "nrms_get_gemm_arith": (_i32, []),
     "nrms_status_string": (ctypes.c_char_p, [_i32]),
     "nrms_last_hip_error": (_i32, []),

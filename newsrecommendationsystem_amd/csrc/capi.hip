@@ -22,7 +22,11 @@ static int initial_gemm_arith() {
   return NRMS_GEMM_SPLIT_F16X3;
 }
 static std::atomic<int> g_gemm_arith{initial_gemm_arith()};
-int gemm_arith() { return g_gemm_arith.load(std::memory_order_relaxed); }
+static thread_local int32_t t_gemm_arith = -1;   // nrms_set_thread_gemm_arith (-1: none)
+int gemm_arith() {
+  const int32_t t = t_gemm_arith;
+  return t >= 0 ? t : g_gemm_arith.load(std::memory_order_relaxed);
+}
 
 void ensure_dynamic_lds(const void* fn, int bytes) {
   static std::mutex mu;
@@ -179,6 +183,24 @@ int32_t nrms_get_gemm_arith(void) { return gemm_arith(); }
 int32_t nrms_set_title_dedupe(int32_t on) { return set_title_dedupe(on); }
 
 int32_t nrms_set_token_compaction(int32_t on) { return set_token_compaction(on); }
+
+int32_t nrms_set_thread_gemm_arith(int32_t mode) {
+  if (mode != -1 && mode != NRMS_GEMM_SPLIT_BF16X6 && mode != NRMS_GEMM_F32 && mode != NRMS_GEMM_SPLIT_F16X3)
+    return -NRMS_ERR_INVALID_ARG;
+  const int32_t prev = t_gemm_arith;
+  t_gemm_arith = mode;
+  return prev;
+}
+
+int32_t nrms_set_thread_title_dedupe(int32_t on) {
+  if (on < -1) return -NRMS_ERR_INVALID_ARG;
+  return set_thread_title_dedupe(on);
+}
+
+int32_t nrms_set_thread_token_compaction(int32_t on) {
+  if (on < -1) return -NRMS_ERR_INVALID_ARG;
+  return set_thread_token_compaction(on);
+}
 
 const char* nrms_status_string(int32_t st) {
   switch (st) {

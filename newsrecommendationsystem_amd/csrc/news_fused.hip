@@ -1295,10 +1295,24 @@ static std::atomic<int> g_token_compaction{[] {
   const char* e = getenv("NRMS_COMPACT");
   return (e && e[0] == '0') ? 0 : 1;
 }()};
-int title_dedupe() { return g_title_dedupe.load(std::memory_order_relaxed); }
+// per-thread overrides (nrms_set_thread_*; -1: none)
+static thread_local int t_title_dedupe = -1, t_token_compaction = -1;
+int title_dedupe() { return t_title_dedupe >= 0 ? t_title_dedupe : g_title_dedupe.load(std::memory_order_relaxed); }
 int set_title_dedupe(int on) { return g_title_dedupe.exchange(on ? 1 : 0); }
-int token_compaction() { return g_token_compaction.load(std::memory_order_relaxed); }
+int token_compaction() {
+  return t_token_compaction >= 0 ? t_token_compaction : g_token_compaction.load(std::memory_order_relaxed);
+}
 int set_token_compaction(int on) { return g_token_compaction.exchange(on ? 1 : 0); }
+int set_thread_title_dedupe(int on) {
+  const int prev = t_title_dedupe;
+  t_title_dedupe = on < 0 ? -1 : (on ? 1 : 0);
+  return prev;
+}
+int set_thread_token_compaction(int on) {
+  const int prev = t_token_compaction;
+  t_token_compaction = on < 0 ? -1 : (on ? 1 : 0);
+  return prev;
+}
 
 bool fused_news_supported(int L, int D, int H, int Q) {
   return L == FL && D == FD && H == FH && Q == FQ;

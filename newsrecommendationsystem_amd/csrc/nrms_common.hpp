@@ -265,6 +265,9 @@ int set_title_dedupe(int on);
 // turns it off).
 int token_compaction();
 int set_token_compaction(int on);
+// per-thread overrides of the two switches above (-1 clears; return the previous override)
+int set_thread_title_dedupe(int on);
+int set_thread_token_compaction(int on);
 
 // workspace of launch_fused_news: packed W_add, special rows, recheck list
 size_t fused_news_workspace_floats(int64_t n_titles);

@@ -76,6 +76,34 @@ def test_gemm_arith_setting_without_gpu():
     assert lib.nrms_get_gemm_arith() == start
 
 
+def test_thread_overrides_of_process_switches():
+    """nrms_set_thread_* (ABI 6): an override applies to the calling host
+    thread only; -1 clears it; the process-wide setting is untouched."""
+    import threading
+    from newsrecommendationsystem_amd import _native as N
+    lib = N.load()
+    start = lib.nrms_get_gemm_arith()
+    seen = {}
+
+    def worker():
+        assert lib.nrms_set_thread_gemm_arith(N.NRMS_GEMM_F32) == -1
+        seen["worker"] = lib.nrms_get_gemm_arith()
+        assert lib.nrms_set_thread_title_dedupe(0) == -1
+        assert lib.nrms_set_thread_token_compaction(0) == -1
+        assert lib.nrms_set_thread_gemm_arith(7) < 0 and lib.nrms_set_thread_title_dedupe(-2) < 0
+        assert lib.nrms_set_thread_gemm_arith(-1) == N.NRMS_GEMM_F32
+        seen["cleared"] = lib.nrms_get_gemm_arith()
+
+    with N.gemm_arith(N.NRMS_GEMM_SPLIT_BF16X6):
+        t = threading.Thread(target=worker)
+        t.start()
+        t.join()
+        assert lib.nrms_get_gemm_arith() == N.NRMS_GEMM_SPLIT_BF16X6   # this thread: process-wide
+        assert seen == {"worker": N.NRMS_GEMM_F32, "cleared": N.NRMS_GEMM_SPLIT_BF16X6}
+    assert lib.nrms_get_gemm_arith() == start
+    assert lib.nrms_set_thread_gemm_arith(-1) == -1   # (never set on this thread)
+
+
 def test_abi_queries_without_gpu():
     from newsrecommendationsystem_amd import _native as N
     lib = N.load()
