@@ -393,37 +393,6 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     if constexpr (MODE == 2) {
       const uf16x8* Bq = reinterpret_cast<const uf16x8*>(WaP) + lane;
       const _Float16* t16 = reinterpret_cast<const _Float16*>(tile);
-#ifdef NRMS_USER_BPRE
-      // one or two live M-tiles: a k-step's 3-6 MFMAs cannot cover its W_add
-      // fragment's L2 latency, so every k-step's fragments are loaded up front
-      if constexpr (MT <= 2 && NTPW == 1) {
-        uf16x8 bp[UKS][2];
-        const int nt = w;
-#pragma unroll
-        for (int ks = 0; ks < UKS; ++ks)
-#pragma unroll
-          for (int pl = 0; pl < 2; ++pl) bp[ks][pl] = Bq[((ks * UNT + nt) * 2 + pl) * 64];
-#pragma unroll
-        for (int ks = 0; ks < UKS; ++ks) {
-          uf16x8 a[MT][2];
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int pl = 0; pl < 2; ++pl)
-              a[mt][pl] = *reinterpret_cast<const uf16x8*>(t16 + 2 * arow[mt] + UKP * pl + 32 * ks + 8 * kq);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            c[mt][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0], bp[ks][1], c[mt][0], 0, 0, 0);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            c[mt][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][1], bp[ks][0], c[mt][0], 0, 0, 0);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            c[mt][0] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0] * (_Float16)kF16LoScale, bp[ks][0], c[mt][0],
-                                                              0, 0, 0);
-        }
-      } else
-#endif
       for (int ks = 0; ks < UKS; ++ks) {
         uf16x8 a[MT][2];
 #pragma unroll
