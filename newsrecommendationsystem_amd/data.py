@@ -136,6 +136,102 @@ def read_behaviors(path):
     return out
 
 
+_DIGITS = str.maketrans("", "", "0123456789")
+
+
+def numeric_news_index(corpus):
+    """int64 array: numeric part of a MIND news id ("N<digits>") -> the id's
+    first corpus row (-1: absent), or None unless every corpus id is exactly
+    "N" followed by digits without a leading zero (so that the number
+    identifies the string)."""
+    ids = corpus.ids
+    if not ids:
+        return None
+    joined = " ".join(ids)
+    n = len(ids)
+    if (joined.translate(_DIGITS) != " ".join(["N"] * n) or joined.count("N0") != joined.count("N0 ") + (
+            1 if joined.endswith("N0") else 0)):
+        return None
+    nums = np.fromstring(joined.replace("N", " "), dtype=np.int64, sep=" ")
+    if nums.size != n:
+        return None
+    uniq, first = np.unique(nums, return_index=True)   # (the first row of a repeated id)
+    index = np.full(int(uniq[-1]) + 1, -1, dtype=np.int64)
+    index[uniq] = first
+    return index
+
+
+def _index_rows(index, ids):
+    """corpus rows of numeric ids (KeyError naming the first unknown id)."""
+    known = ids < index.size
+    rows = np.full(ids.size, -1, dtype=np.int64)
+    rows[known] = index[ids[known]]
+    if (rows < 0).any():
+        raise KeyError("N%d" % int(ids[int(np.argmax(rows < 0))]))
+    return rows
+
+
+def candidate_rows_numeric(impressions, index):
+    """(corpus rows int64, labels int32, per-impression counts) of every
+    candidate of a split, in order, by one numeric parse of the joined raw
+    cells -- or None unless every cell is single-space separated
+    "N<digits>-<digits>" tokens (no leading zeros in the ids), the form whose
+    parse equals the per-token split('-') and news2vector[...] lookup of
+    src/evaluate.py:153-157,251-255. An id missing from the corpus raises
+    KeyError as the dict does."""
+    n = len(impressions)
+    raws = [im.raw for im in impressions]
+    if index is None or not n or any(r is None or r == "" for r in raws):
+        return None
+    joined = "\n".join(raws)
+    buf = np.frombuffer(joined.encode("ascii", "replace"), dtype=np.uint8)
+    seps = np.flatnonzero((buf == 32) | (buf == 10))
+    ntok = seps.size + 1
+    # the digit-free skeleton must be exactly "N- N- ... N-" (one line per impression)
+    if joined.replace("\n", " ").translate(_DIGITS) != " ".join(["N-"] * ntok):
+        return None
+    if joined.count("N0") != joined.count("N0-"):   # (a leading zero: the string is not the number's)
+        return None
+    vals = np.fromstring(joined.replace("N", " ").replace("-", " "), dtype=np.int64, sep=" ")
+    if vals.size != 2 * ntok:
+        return None
+    # tokens per impression: the separators before each line break, + 1
+    is_nl = buf[seps] == 10
+    ends = np.append(np.flatnonzero(is_nl), seps.size)          # separator index of each line's end
+    counts = np.diff(np.concatenate([[-1], ends])).astype(np.int64)
+    return _index_rows(index, vals[0::2]), vals[1::2].astype(np.int32), counts
+
+
+def history_rows_numeric(histories, index, num_clicked, pad_row):
+    """[len(histories), num_clicked] corpus rows of each history's first
+    num_clicked ids, left-padded with pad_row (history_ids +
+    news2vector[...], src/evaluate.py:115-124) -- or None unless every
+    history is single-space separated "N<digits>" ids (no leading zeros) or
+    blank."""
+    if index is None:
+        return None
+    hs = [h.strip() for h in histories]
+    cnt = np.fromiter((h.count("N") for h in hs), dtype=np.int64, count=len(hs))
+    total = int(cnt.sum())
+    rows = np.full((len(hs), num_clicked), pad_row, dtype=np.int64)
+    if total == 0:
+        return rows if all(h == "" for h in hs) else None
+    joined = " ".join(h for h in hs if h)
+    if joined.translate(_DIGITS) != " ".join(["N"] * total):
+        return None
+    if joined.count("N0") != joined.count("N0 ") + (1 if joined.endswith("N0") else 0):
+        return None
+    nums = np.fromstring(joined.replace("N", " "), dtype=np.int64, sep=" ")
+    if nums.size != total:
+        return None
+    m = np.minimum(cnt, num_clicked)                 # ids kept per history (the first m)
+    off = np.cumsum(cnt) - cnt                       # first id of each history in nums
+    u = np.repeat(np.arange(len(hs)), m)
+    k = np.arange(int(m.sum())) - np.repeat(np.cumsum(m) - m, m)
+    rows[u, num_clicked - np.repeat(m, m) + k] = _index_rows(index, nums[np.repeat(off, m) + k])
+    return rows
+
+
 def parse_impression_cells(impressions):
     """(candidate ids, labels int32, per-impression counts) of a split, in
     order. One split of the joined raw cells when every token is `<id>-<label>`

@@ -24,7 +24,8 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .data import PADDED_NEWS, history_ids, parse_impression_cells, read_behaviors, read_news_parsed
+from .data import (PADDED_NEWS, candidate_rows_numeric, history_ids, history_rows_numeric, numeric_news_index,
+                   parse_impression_cells, read_behaviors, read_news_parsed)
 
 
 class EvalPlan:
@@ -53,21 +54,31 @@ class EvalPlan:
                 u = hist_of[im.clicked_news] = len(hists)
                 hists.append(im.clicked_news)
             imp_user[k] = u
-        cand_names, self.labels, counts = parse_impression_cells(self.impressions)
         rows_of = corpus.index   # news id -> first row (news2vector[...], evaluate.py:255)
 
         def lookup(names):
             return np.fromiter(map(rows_of.__getitem__, names), dtype=np.int64, count=len(names))
 
-        self.cand = lookup(cand_names).astype(np.int64) if cand_names else np.zeros(0, np.int64)
+        # MIND-form cells ("N<digits>-<label>"): one numeric parse and an array
+        # index (data.candidate_rows_numeric); any other form: the per-name path
+        nindex = numeric_news_index(corpus)
+        fast = candidate_rows_numeric(self.impressions, nindex)
+        if fast is not None:
+            self.cand, self.labels, counts = fast
+        else:
+            cand_names, self.labels, counts = parse_impression_cells(self.impressions)
+            self.cand = lookup(cand_names).astype(np.int64) if cand_names else np.zeros(0, np.int64)
         self.pair_user = np.repeat(imp_user, counts)
         self.offsets = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
-        hist_names = [x for h in hists for x in history_ids(h, num_clicked)]
-        real = np.array([x != PADDED_NEWS for x in hist_names], dtype=bool)
-        rows = np.full(len(hist_names), pad, dtype=np.int64)
-        if real.any():
-            rows[real] = lookup([x for x, r in zip(hist_names, real) if r])
-        self.hist_rows = rows.reshape(len(hists), num_clicked)
+        hrows = history_rows_numeric(hists, nindex, num_clicked, pad)
+        if hrows is None:
+            hist_names = [x for h in hists for x in history_ids(h, num_clicked)]
+            real = np.array([x != PADDED_NEWS for x in hist_names], dtype=bool)
+            rows = np.full(len(hist_names), pad, dtype=np.int64)
+            if real.any():
+                rows[real] = lookup([x for x, r in zip(hist_names, real) if r])
+            hrows = rows.reshape(len(hists), num_clicked)
+        self.hist_rows = hrows
         self.num_clicked = num_clicked
 
     @property
