@@ -20,7 +20,7 @@
 //      conflict-free at row stride 600 floats), W_add pre-split into bf16
 //      planes packed in the same K order; or exact f32 MFMA 16x16x4 (MODE 0). Wave w owns N-tiles w, w + NW, ...
 //      for all M-tiles (rows >= N read row N-1 and are dropped). Epilogue:
-//      per-row partials of q_n tanh(y + b_n), one LDS row per N-tile;
+//      per-row partials of q_n tanh(y + b_n) (v_exp + v_rcp form), one LDS row per N-tile;
 //   3. softmax over the N rows (max-subtracted, F.softmax) and the pooling
 //      (two lanes per float4 column, combined by a lane shuffle).
 // MODE 2 (split-f16, the default arithmetic): each context row is scaled by
@@ -72,14 +72,6 @@ static_assert(pk::KS == UKS && pk::NT == UNT && pk::KG == UKG && pk::Q == UQ && 
                   pk::USER_F32_ELEMS == UWAP1,
               "packs.hpp layout");
 static_assert(pk::USER_H3_EXP + pk::NT * 16 <= UWAP_MAX, "split-f16 W_add pack fits the workspace");
-
-__device__ __forceinline__ float urow16_sum(float v) {
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x4E, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x141, 0xF, 0xF, false));
-  v += __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x140, 0xF, 0xF, false));
-  return v;
-}
 
 constexpr int URS = 2 * UD;                // LDS row stride: K|V, then context (conflict-free)
 constexpr int UKP = 320;                   // bf16 context plane width (K padded)
@@ -470,8 +462,14 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     for (int j = 0; j < NTPW; ++j) {
       const int nt = w + NW * j;
       if (nt >= UNT) break;
+      // q tanh(y + b) = q - 2q / (e^(2(y + b)) + 1): v_exp_f32 + v_rcp_f32
+      // (absolute error ~1e-7, as the news kernel's epilogue; saturates,
+      // propagates NaN); the four rows' DPP sums stage by stage
+      constexpr float kC2 = 2.8853900817779268f;   // 2 log2(e)
+      const float cb = kC2 * bv[j], m2q = -2.0f * qv[j];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
+        float p[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float y = c[mt][j][r];
@@ -479,9 +477,16 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
             const int row = 16 * mt + 4 * kq + r;
             y = ldexpf(y, rexp[row < L ? row : L - 1] + ewv[j] - 11);
           }
-          const float p = urow16_sum(qv[j] * tanhf(y + bv[j]));
-          if (lm == 0) part[nt * 64 + 16 * mt + 4 * kq + r] = p;
+          p[r] = fmaf(m2q, __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(fmaf(y, kC2, cb)) + 1.0f), qv[j]);
         }
+#define NRMS_UDPP4(CTRL)                                                                                  \
+  _Pragma("unroll") for (int r = 0; r < 4; ++r) p[r] += __builtin_bit_cast(                              \
+      float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, p[r]), CTRL, 0xF, 0xF, false));
+        NRMS_UDPP4(0xB1) NRMS_UDPP4(0x4E) NRMS_UDPP4(0x141) NRMS_UDPP4(0x140)
+#undef NRMS_UDPP4
+        if (lm == 0)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) part[nt * 64 + 16 * mt + 4 * kq + r] = p[r];
       }
     }
   };
