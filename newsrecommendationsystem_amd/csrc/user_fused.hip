@@ -22,7 +22,7 @@
 //      for all M-tiles (rows >= N read row N-1 and are dropped). Epilogue:
 //      per-row partials of q_n tanh(y + b_n) (v_exp + v_rcp form), one LDS row per N-tile;
 //   3. softmax over the N rows (max-subtracted, F.softmax) and the pooling
-//      (two lanes per float4 column, combined by a lane shuffle).
+//      (up to eight lanes per float4 column, combined by lane shuffles).
 // MODE 2 (split-f16, the default arithmetic): each context row is scaled by
 // a power of two, 2^-ea (its max |value| into [2^3, 2^4): each (head,
 // query) thread leaves its max in an LDS slot, read by the row's 15 threads
@@ -515,12 +515,15 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   }
   __syncthreads();
   NRMS_U_STAMP(4)   // softmax
-  // two lanes per float4 column (rows of one parity each), 150 lanes in 3 waves
-  if (tid < 192) {
-    const int u = tid >> 1, par = tid & 1;
+  // PP lanes per float4 column (rows i = par mod PP each), combined by lane
+  // shuffles: 8 per column (600 lanes) when the workgroup has them
+  constexpr int PP = NT >= 8 * (UD / 4) ? 8 : (NT >= 4 * (UD / 4) ? 4 : 2);
+  constexpr int PT = (PP * (UD / 4) + 63) / 64 * 64;
+  if (tid < PT) {
+    const int u = tid / PP, par = tid % PP;
     float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
     if (u < UD / 4) {
-      for (int i = par; i < L; i += 2) {
+      for (int i = par; i < L; i += PP) {
         const float wi = wts[i];
         float4 cv;
         if constexpr (MODE == 2) {   // ldexp(hi + 2^-11 (lo + r), ea): the fp32 context (see MODE 2)
@@ -552,10 +555,13 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         o.w = fmaf(wi, cv.w, o.w);
       }
     }
-    o.x += __shfl_xor(o.x, 1);
-    o.y += __shfl_xor(o.y, 1);
-    o.z += __shfl_xor(o.z, 1);
-    o.w += __shfl_xor(o.w, 1);
+#pragma unroll
+    for (int m = 1; m < PP; m <<= 1) {
+      o.x += __shfl_xor(o.x, m);
+      o.y += __shfl_xor(o.y, m);
+      o.z += __shfl_xor(o.z, m);
+      o.w += __shfl_xor(o.w, m);
+    }
     if (u < UD / 4 && par == 0) reinterpret_cast<float4*>(out + s * UD)[u] = o;
   }
 #ifdef NRMS_USER_TIMING
