@@ -384,6 +384,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend for the barrier / max-over-ranks timing (nccl = RCCL); "
                          "gloo lets several ranks share one GPU for a rehearsal")
+    ap.add_argument("--init-dist", action="store_true",
+                    help="initialise the process group (and take the barrier / max-over-ranks path) even "
+                         "at world size 1: the RCCL code path on one GPU (tests)")
     ap.add_argument("--dump-logits", default=None, metavar="PATH",
                     help="after the timed region, score every batch once more and save this rank's "
                          "impression indices and logits to PATH.rank<r>.npz (multi-rank tests)")
@@ -400,7 +403,7 @@ def main():
     device = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(device)
     dist = None
-    if world > 1:
+    if world > 1 or args.init_dist:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
@@ -502,11 +505,8 @@ def main():
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        if args.dist_backend != "nccl":
-            t = t.cpu()
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        from newsrecommendationsystem_amd.distributed import max_over_ranks
+        elapsed = max_over_ranks(elapsed, device)
 
     if args.dump_logits:
         # untimed: every batch of this rank's shard once, logits by impression index
@@ -545,8 +545,11 @@ def main():
     n_clk = clk.shape[0] * N_CLICKED
     clk_pad = int(pad[:n_clk].sum())
     n_user = n_clk - max(clk_pad - 1, 0) if not args.unfused else n_clk
-    # UserEncoder rows: every user on its N clicked positions
-    user_rows = (n_clk, clk.shape[0] * N_CLICKED * N_CLICKED)
+    # UserEncoder rows: with compaction a user is encoded on Le = real + (1 if
+    # any padding) rows (fused_user_kernel, UF_COMPACT), else on N
+    real = (~pad[:n_clk]).view(-1, N_CLICKED).sum(-1)
+    ule = torch.where(real < N_CLICKED, real + 1, real) if compact else torch.full_like(real, N_CLICKED)
+    user_rows = (int(ule.sum()), int((ule * ule).sum()))
     work = (plan.work(titles_encoded=n_enc, user_rows_projected=n_user, news_rows=news_rows,
                       user_rows=user_rows) if not args.unfused else plan.work())
     dom = max(stage_ms, key=stage_ms.get)
@@ -562,11 +565,8 @@ def main():
     if args.stream:
         done = (steps * B + (tail[0][0].shape[0] if tail and steps == len(full) else 0))
         if dist:
-            tt = torch.tensor([float(done)], dtype=torch.float64, device=device)
-            if args.dist_backend != "nccl":
-                tt = tt.cpu()
-            dist.all_reduce(tt)
-            done = float(tt.item())
+            from newsrecommendationsystem_amd.distributed import sum_over_ranks
+            done = sum_over_ranks(done, device)
         value = done / elapsed
     else:
         value = world * B * steps / elapsed

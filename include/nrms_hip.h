@@ -137,11 +137,14 @@ int32_t nrms_set_title_dedupe(int32_t on);
  * title (its right-padding, src/data_preprocess.py:115,132-139) share one
  * q|k|v row, so a title with c real tokens is encoded on c + 1 distinct rows,
  * the padding row carrying its multiplicity 20 - c in the raw-exp sums, the
- * attention context and the additive softmax / pooling (news_fused.hip). The
- * raw-exp row sums are bitwise the uncompacted ones (the padding row's exp is
- * added 20 - c times, in the reference's key order); the context and pooling
- * replace 20 - c equal additions by one product: results agree with the
- * uncompacted computation to fp32 rounding. Process-wide, read at enqueue
+ * attention context and the additive softmax / pooling (news_fused.hip). For
+ * right-padded titles (all id-0 tokens after the real ones) the raw-exp row
+ * sums are bitwise the uncompacted ones (the padding row's exp is added
+ * 20 - c times, in the reference's key order). An id-0 token in the middle
+ * of a title (an out-of-vocabulary word, src/data_preprocess.py:134-135) is
+ * summed after the real keys instead, so its row sums agree only to fp32
+ * rounding. The context and pooling replace 20 - c equal additions by one
+ * product: results agree with the uncompacted computation to fp32 rounding. Process-wide, read at enqueue
  * time; returns the previous setting. NRMS_COMPACT=0 in the environment
  * starts with it off. */
 int32_t nrms_set_token_compaction(int32_t on);

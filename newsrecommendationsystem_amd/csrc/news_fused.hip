@@ -179,9 +179,11 @@ static_assert(pk::NEWS_COUNTERS == WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS, "pack
 // that carries the multiplicity n_pad:
 //   raw-exp sums  sum_k e_k: the real keys, the rep, then n_pad - 1 more
 //                 additions of the rep's e, in that order (the reference's key
-//                 order for right padding; the sum, and with it the overflow /
+//                 order for right padding: the sum, and with it the overflow /
 //                 NaN behaviour of multihead_self.py:16-20, is bitwise the
-//                 uncompacted one);
+//                 uncompacted one when all padding is trailing; an interior
+//                 id-0 token -- an OOV word, src/data_preprocess.py:134-135 --
+//                 moves to the end of the sum, fp32-rounding-level);
 //   context       ctx = sum_k P_k v_k with the rep's P scaled by n_pad;
 //   softmax/pool  the rep's score and context row weighted by n_pad
 //                 (additive.py:37-52).

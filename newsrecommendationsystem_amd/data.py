@@ -105,6 +105,8 @@ class Impression:
 
     @candidates.setter
     def candidates(self, v):
+        if self._labels is None and self.raw is not None:
+            self._parse()
         self._cands, self.raw = v, None
 
     @property
@@ -143,12 +145,16 @@ def numeric_news_index(corpus):
     """int64 array: numeric part of a MIND news id ("N<digits>") -> the id's
     first corpus row (-1: absent), or None unless every corpus id is exactly
     "N" followed by digits without a leading zero (so that the number
-    identifies the string)."""
+    identifies the string). Also None (the per-name dict path) when an id has
+    more than 18 digits (past int64's exact parse) or the largest number is
+    far beyond the corpus size (the dense index would be mostly empty)."""
     ids = corpus.ids
     if not ids:
         return None
-    joined = " ".join(ids)
     n = len(ids)
+    if max(map(len, ids)) > 19:
+        return None
+    joined = " ".join(ids)
     if (joined.translate(_DIGITS) != " ".join(["N"] * n) or joined.count("N0") != joined.count("N0 ") + (
             1 if joined.endswith("N0") else 0)):
         return None
@@ -156,6 +162,8 @@ def numeric_news_index(corpus):
     if nums.size != n:
         return None
     uniq, first = np.unique(nums, return_index=True)   # (the first row of a repeated id)
+    if int(uniq[-1]) > 16 * n + (1 << 20):
+        return None
     index = np.full(int(uniq[-1]) + 1, -1, dtype=np.int64)
     index[uniq] = first
     return index

@@ -49,6 +49,29 @@ def all_reduce_(t, group=None):
     return t
 
 
+def _reduce_scalar(x, device, op, group=None):
+    """One fp64 scalar reduced over the group: on the device under RCCL
+    ("nccl"), through host memory under gloo."""
+    import torch.distributed as dist
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    if dist.get_backend(group) != "nccl":
+        t = t.cpu()
+    dist.all_reduce(t, op=op, group=group)
+    return float(t.item())
+
+
+def max_over_ranks(x, device, group=None):
+    """MAX of a per-rank scalar (bench.py: the timed region's wall time)."""
+    import torch.distributed as dist
+    return _reduce_scalar(x, device, dist.ReduceOp.MAX, group)
+
+
+def sum_over_ranks(x, device, group=None):
+    """SUM of a per-rank scalar (bench.py --stream: impressions scored)."""
+    import torch.distributed as dist
+    return _reduce_scalar(x, device, dist.ReduceOp.SUM, group)
+
+
 def shard_rows(n, rank, world):
     """Contiguous [start, stop) slice of n independent units for weak/strong
     scaling of synthetic batches."""

@@ -71,6 +71,10 @@ class ForwardPlan:
         if self.user_fused:
             nb = lib.nrms_user_attention_pool_workspace_size(B, n_clicked, D)
             self.uws = torch.empty(nb, dtype=torch.uint8, device=self.dev)
+            # the clicked positions' all-padding flags, computed into these
+            # buffers before the first stage event (no allocation per call)
+            self._eq = torch.empty(B, n_clicked, L, dtype=torch.bool, device=self.dev)
+            self._pad = torch.empty(B, n_clicked, dtype=torch.bool, device=self.dev)
 
     def run(self, cand_ids, clicked_ids, events=None):
         """cand_ids [B,C,L], clicked_ids [B,N,L] int64 on the device. If
@@ -82,6 +86,11 @@ class ForwardPlan:
         wn, wu = ctypes.byref(self.wn), ctypes.byref(self.wu)
         P = N.ptr
         rec = (lambda i: events[i].record()) if events is not None else (lambda i: None)
+        if self.user_fused:
+            # the clicked positions holding all-padding titles (one news vector):
+            # the user tail compacts them as nrms_forward does (token compaction)
+            torch.eq(clicked_ids, 0, out=self._eq)
+            torch.all(self._eq, dim=-1, out=self._pad)
 
         rec(0)
         ldq, uldq = self.ldq, self.uldq
@@ -113,10 +122,7 @@ class ForwardPlan:
         N.call("nrms_qkv_project_ws", P(self.news), n_clk, None, n_clk, wu, P(self.uqkv), uldq, pws, npws, st)
         rec(k + 1)
         if self.user_fused:
-            # the clicked positions holding all-padding titles (one news vector):
-            # the tail compacts them as nrms_forward does (token compaction)
-            pad = (clicked_ids == 0).all(-1).to(torch.uint8).contiguous()
-            N.call("nrms_user_attention_pool_padded", P(self.uqkv), uldq, B, Nc, P(pad), wu, P(self.user),
+            N.call("nrms_user_attention_pool_padded", P(self.uqkv), uldq, B, Nc, P(self._pad), wu, P(self.user),
                    P(self.uws), self.uws.numel(), st)
             k += 1
         else:

@@ -34,11 +34,11 @@ from .evaluate import EvalPlan, evaluate, score_plan
 from .nrms import NRMS
 
 
-def make_config(V, lr=2e-3):
-    """NRMSConfig for the planted-teacher runs: vocabulary V, dropout 0 (no RNG
-    in the step), learning rate lr (the reference's 1e-4 moves a random
-    student too little in a few dozen steps to say anything about AUC)."""
-    return type("QualityCfg", (NRMSConfig,), dict(num_words=V, dropout_probability=0.0, learning_rate=lr))
+def make_config(V, lr=2e-3, dropout=0.0):
+    """NRMSConfig for the planted-teacher runs: vocabulary V, dropout (0: no
+    RNG in the step), learning rate lr (the reference's 1e-4 moves a random
+    student too little in a few hundred steps to say anything about AUC)."""
+    return type("QualityCfg", (NRMSConfig,), dict(num_words=V, dropout_probability=dropout, learning_rate=lr))
 
 
 def model_from_seed(cfg, seed):
@@ -158,3 +158,128 @@ def run(steps=32, every=4, world=2, B=16, C=3, seed=0, cpu=True):
                         "max_normwise_param_diff_hip_vs_cpu_excl_WK_bias": diff,
                         "mrr_hip": auc_hip[1], "mrr_cpu": auc_cpu[1]})
         return out
+
+
+# ---------------------------------------------------------------- config 5 at scale
+def teacher_batches_device(teacher, titles, seed, n_batches, B, C=3, N=50):
+    """teacher_batches on the device (titles: int64 [n_news, 20] there): per
+    row U{1..N} clicked news left-padded with all-zero titles
+    (src/dataset.py:79-83) and C candidates ordered by the teacher's score,
+    positive first (src/train.py:205-206)."""
+    dev = titles.device
+    g = torch.Generator(device=dev).manual_seed(seed)
+    n_news, L = titles.shape
+    out = []
+    for _ in range(n_batches):
+        cand = titles[torch.randint(0, n_news, (B, C), generator=g, device=dev)]
+        clk = titles[torch.randint(0, n_news, (B, N), generator=g, device=dev)]
+        hist = torch.randint(1, N + 1, (B, 1), generator=g, device=dev)
+        clk = torch.where((torch.arange(N, device=dev)[None] < (N - hist))[:, :, None], torch.zeros_like(clk), clk)
+        with torch.no_grad():
+            y = teacher.forward_ids(cand, clk)
+        order = torch.argsort(-y, dim=1, stable=True)
+        cand = torch.gather(cand, 1, order[:, :, None].expand(-1, -1, L))
+        out.append((cand.contiguous(), clk.contiguous()))
+    return out
+
+
+def _fedavg_(models):
+    """Replace every client's parameters by the clients' mean (train.FedAvg's
+    exchange: sum over clients / count)."""
+    with torch.no_grad():
+        for ps in zip(*[list(m.parameters()) for m in models]):
+            acc = ps[0].detach().clone()
+            for p in ps[1:]:
+                acc += p.detach()
+            acc /= len(ps)
+            for p in ps:
+                p.copy_(acc)
+
+
+def train_clients_reference(init, client_batches, every, device):
+    """The same FedAvg schedule on the reference's op sequence (train.py:
+    forward_autograd, ATen autograd, CrossEntropy vs class 0) with
+    torch.optim.Adam, on `device`. With dropout p > 0 the step takes the HIP
+    step's dropout sample: its masks come from the HIP generator with the same
+    per-call seed the HIP student uses (1, 2, ... per client, NRMS.forward_ids)
+    and enter as explicit multiplicative masks (train.forward_autograd_masked)."""
+    models = [copy.deepcopy(init).to(device) for _ in client_batches]
+    opts = [torch.optim.Adam(m.parameters(), lr=m.config.learning_rate) for m in models]
+    p = float(init.config.dropout_probability)
+    steps = len(client_batches[0])
+    t_steps = 0.0
+    for k in range(steps):
+        for m, opt, batches in zip(models, opts, client_batches):
+            cand, clk = (t.to(device) for t in batches[k])
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            t0 = time.perf_counter()
+            m.train()
+            if p > 0:
+                B, C, L = cand.shape
+                masks = TR.hip_dropout_masks(B * (C + clk.shape[1]) * L, 300, p, k + 1, device)
+                logits = TR.forward_autograd_masked(m, cand, clk, masks)
+            else:
+                logits = TR.forward_autograd(m, cand, clk, training=False)
+            loss = TR.loss_fn(logits)
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+            if device.type == "cuda":
+                torch.cuda.synchronize(device)
+            t_steps += time.perf_counter() - t0
+        if every > 0 and (k + 1) % every == 0:
+            _fedavg_(models)
+    return models[0], t_steps, steps
+
+
+def run_scaled(steps=320, every=10, world=2, B=128, C=3, V=70976, n_news=20000, dropouts=(0.0, 0.2),
+               lr=1e-3, seed=0, temperature=0.5, eval_impressions=4000):
+    """BASELINE config 5's quality half at the reference's dimensions: V =
+    70,976 words, batch 128 (src/config.py:18), 1 + K = 3 candidates, 50
+    clicked, `world` FedAvg clients x `steps` local steps, parameters averaged
+    every `every` steps; the HIP student (HIP training kernels + HipAdam)
+    against the reference student (the reference's op sequence on ATen
+    autograd + torch.optim.Adam, on the GPU as src/train.py:24 selects when
+    one is present), both from one initialisation on the same batches, both
+    evaluated with evaluate() on a planted-teacher split. One run per dropout
+    probability; with p > 0 the reference student takes the HIP masks."""
+    dev = torch.device("cuda")
+    res = {"workload": (f"planted teacher: {world} FedAvg clients x {steps} local steps, batch {B}, 1+K={C}, "
+                        f"50 clicked, V={V}, {n_news} news, lr {lr}, FedAvg every {every} steps; eval split "
+                        f"{eval_impressions} impressions, labels ~ Bernoulli(sigmoid(teacher logit / {temperature}))"),
+           "reference_path": "src/train.py loop body on ATen autograd + torch.optim.Adam, on the GPU "
+                             "(src/train.py:24 device selection)",
+           "runs": []}
+    with tempfile.TemporaryDirectory() as d:
+        cfg0 = make_config(V, lr)
+        teacher = model_from_seed(cfg0, 1000 + seed).to(dev).eval()
+        corpus, imps = Dt.synthetic_split(d, seed=seed, n_news=n_news, n_users=3000,
+                                          n_impressions=eval_impressions, V=V,
+                                          teacher=teacher_logits_fn(teacher), temperature=temperature)
+        titles = torch.from_numpy(np.asarray(corpus.titles, dtype=np.int64)).to(dev)
+        client_batches = [teacher_batches_device(teacher, titles, 100 + 17 * r + seed, steps, B, C)
+                          for r in range(world)]
+        for p in dropouts:
+            cfg = make_config(V, lr, dropout=p)
+            torch.manual_seed(2000 + seed)
+            student = NRMS(cfg, torch.randn(V, 300) * 0.5)
+            init_auc = auc_of(student.state_dict(), cfg, d)
+            hip, t_hip, n = train_clients(student, client_batches, every, dev)
+            hip_sd = {k: v.detach().cpu() for k, v in hip.state_dict().items()}
+            del hip
+            ref, t_ref, _ = train_clients_reference(student, client_batches, every, dev)
+            ref_sd = {k: v.detach().cpu() for k, v in ref.state_dict().items()}
+            del ref
+            a_hip, a_ref = auc_of(hip_sd, cfg, d), auc_of(ref_sd, cfg, d)
+            diff = max(float((hip_sd[k] - ref_sd[k]).norm() / ref_sd[k].norm().clamp_min(1e-30))
+                       for k in ref_sd if not k.endswith("W_K.bias"))
+            res["runs"].append({
+                "dropout": p, "auc_init": init_auc[0], "auc_hip": a_hip[0], "auc_reference": a_ref[0],
+                "auc_lift_hip": a_hip[0] - init_auc[0], "abs_diff_auc": abs(a_hip[0] - a_ref[0]),
+                "tolerance": 0.002, "mrr_hip": a_hip[1], "mrr_reference": a_ref[1],
+                "max_normwise_param_diff_excl_WK_bias": diff,
+                "hip_train_steps_per_s": round(world * n / t_hip, 1),
+                "reference_train_steps_per_s": round(world * n / t_ref, 1)})
+            torch.cuda.empty_cache()
+    return res

@@ -1,0 +1,16 @@
+"""Exploration of the config-5 planted-teacher settings (quality.run_scaled):
+prints one JSON line per setting. python profiles/probes/quality_probe.py"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+from newsrecommendationsystem_amd import quality as Q  # noqa: E402
+
+for kw in [dict(steps=320, lr=1e-3, temperature=0.5, dropouts=(0.0, 0.2))]:
+    t0 = time.time()
+    r = Q.run_scaled(**kw)
+    r["wall_s"] = round(time.time() - t0, 1)
+    r["kw"] = {k: list(v) if isinstance(v, tuple) else v for k, v in kw.items()}
+    print(json.dumps(r), flush=True)

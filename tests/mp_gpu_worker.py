@@ -4,7 +4,7 @@ MASTER_PORT in the environment), all ranks on cuda:0, collectives on gloo
 (RCCL cannot put two ranks on one GPU). Writes its results as .npy / .json
 files into the output directory given on the command line.
 
-    python tests/mp_gpu_worker.py eval|fedavg|quality OUT_DIR
+    python tests/mp_gpu_worker.py eval|fedavg|quality|collectives OUT_DIR [gloo|nccl]
 """
 import json
 import os
@@ -113,13 +113,54 @@ def run_quality(rank, world, out):
         json.dump({"steps": int(b["cand"].shape[0]), "optimizer": type(opt).__name__}, f)
 
 
+def run_collectives(rank, world, out):
+    """The RCCL code paths of the product on a process group of this worker's
+    backend (test_rccl_world1_collectives: "nccl" = RCCL, world size 1 on
+    cuda:0, against the same calls on gloo): the bench's MAX timing
+    all-reduce (fp64 GPU tensor) and stream-count SUM, evaluate()'s metric
+    all-reduce over user shards, and FedAvg.sync of the HIP-trained
+    parameters."""
+    from newsrecommendationsystem_amd import train as TR
+    from newsrecommendationsystem_amd.distributed import all_reduce_, max_over_ranks, sum_over_ranks
+    from newsrecommendationsystem_amd.evaluate import evaluate
+    dev = torch.device("cuda:0")
+    res = {"backend": dist.get_backend()}
+    res["max"] = max_over_ranks(1.25 + rank, dev)
+    res["sum"] = sum_over_ranks(4096.0 * (rank + 1), dev)
+    t = torch.arange(6, dtype=torch.float32, device=dev) * (rank + 1)
+    res["all_reduce"] = all_reduce_(t).cpu().tolist()
+    g = np.load(os.path.join(ROOT, "tests", "golden", "nrms_flow_golden.npz"))
+    d = os.path.join(ROOT, "tests", "golden", "flow", "eval")
+    V = int(g["V_eval"])
+    m = _model(W.nrms_state(int(g["seed"]), V), V).eval()
+    res["eval_group"] = list(evaluate(m, d, process_group=dist.group.WORLD))
+    res["eval_plain"] = list(evaluate(m, d))
+    V2, B = 2000, 8
+    mt = _model(W.nrms_state(77, V2), V2, dropout_probability=0.2).train()
+    opt = TR.make_optimizer(mt)
+    fed = TR.FedAvg(mt, every=2)
+    for cand, clk in TR.synthetic_train_batches(300 + rank, 2, B, V2, device="cuda:0"):
+        TR.train_step(mt, opt, cand, clk)
+        if fed.steps == 1:
+            pre = torch.cat([p.detach().reshape(-1) for p in mt.parameters()]).cpu().numpy()
+        res.setdefault("synced", []).append(fed.step())
+    post = torch.cat([p.detach().reshape(-1) for p in mt.parameters()]).cpu().numpy()
+    np.save(os.path.join(out, f"rank{rank}_pre.npy"), pre)
+    np.save(os.path.join(out, f"rank{rank}_post.npy"), post)
+    with open(os.path.join(out, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+
+
 def main():
     mode, out = sys.argv[1], sys.argv[2]
+    backend = sys.argv[3] if len(sys.argv) > 3 else "gloo"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     try:
-        {"eval": run_eval, "fedavg": run_fedavg, "quality": run_quality}[mode](rank, world, out)
+        {"eval": run_eval, "fedavg": run_fedavg, "quality": run_quality,
+         "collectives": run_collectives}[mode](rank, world, out)
         dist.barrier()
     finally:
         dist.destroy_process_group()

@@ -146,7 +146,8 @@ def test_numeric_plan_equals_per_name_plan(split, monkeypatch, num_clicked):
     arrays as the per-name dict lookups of src/evaluate.py:115-124,251-255."""
     d, corpus, _ = split
     assert Dt.numeric_news_index(corpus) is not None
-    imps = Dt.read_behaviors(d + "/behaviors.tsv") + [   # (the raw cells as read from the file)Dt.Impression("x1", "U9", "t", " ", ["N3", "N0"], [0, 1], raw="N3-0 N0-1"),
+    imps = Dt.read_behaviors(d + "/behaviors.tsv") + [   # (the raw cells as read from the file)
+        Dt.Impression("x1", "U9", "t", " ", ["N3", "N0"], [0, 1], raw="N3-0 N0-1"),
                    Dt.Impression("x2", "U9", "t", "N7 N8 N0", ["N7"], [1], raw="N7-1")]
     idx = Dt.numeric_news_index(corpus)
     hists = list(dict.fromkeys(im.clicked_news for im in imps))
@@ -179,4 +180,31 @@ def test_numeric_paths_fall_back_or_raise():
     assert Dt.history_rows_numeric(["N1  N5"], idx, 2, 9) is None   # (split() semantics kept by the per-name path)
     with pytest.raises(KeyError):
         Dt.history_rows_numeric(["N1 N7"], idx, 2, 9)
+
+
+def test_sparse_large_numeric_ids_take_the_dict_path(tmp_path):
+    """Ids far beyond the corpus size (or past int64's exact parse) must not
+    build a dense index: numeric_news_index returns None and the per-name
+    plan is used (a sparse 'N9999999999' corpus allocated ~80 GB)."""
+    big = ["N9999999999", "N1", "N123456789012"]
+    assert Dt.numeric_news_index(Dt.NewsCorpus(big, np.zeros((3, 20), np.int64))) is None
+    huge = ["N" + "9" * 25, "N2"]                         # would overflow int64
+    assert Dt.numeric_news_index(Dt.NewsCorpus(huge, np.zeros((2, 20), np.int64))) is None
+    titles = np.arange(3 * 20, dtype=np.int64).reshape(3, 20)
+    corpus = Dt.NewsCorpus(big, titles)
+    imps = [Dt.Impression("1", "U1", "t", "N1 N9999999999", raw="N123456789012-1 N1-0")]
+    plan = EvalPlan(corpus, imps, num_clicked=3)
+    assert plan.cand.tolist() == [2, 1] and plan.labels.tolist() == [1, 0]
+    assert plan.hist_rows.tolist() == [[len(corpus), 1, 0]]
+
+
+def test_impression_setters_keep_the_other_field():
+    """Setting candidates (or labels) on an Impression read from a raw cell
+    parses the cell first, so the other field stays readable."""
+    im = Dt.Impression("1", "U1", "t", " ", raw="N1-1 N2-0")
+    im.candidates = ["N7", "N8"]
+    assert im.labels == [1, 0] and im.candidates == ["N7", "N8"]
+    im = Dt.Impression("1", "U1", "t", " ", raw="N1-1 N2-0")
+    im.labels = [0, 0]
+    assert im.candidates == ["N1", "N2"] and im.labels == [0, 0]
 

@@ -26,13 +26,13 @@ def _free_port():
     return p
 
 
-def _run(mode, out, world=2, timeout=240):
+def _run(mode, out, world=2, timeout=240, backend="gloo"):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, "-u", WORKER, mode, str(out)], env=env,
+        procs.append(subprocess.Popen([sys.executable, "-u", WORKER, mode, str(out), backend], env=env,
                                       stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     logs = []
     try:
@@ -165,3 +165,58 @@ def test_fedavg_training_quality_hip_vs_cpu(tmp_path):
             continue
         rel = float((hip_sd[k] - cpu_sd[k]).norm() / cpu_sd[k].norm().clamp_min(1e-30))
         assert rel < 1e-3, (k, rel)
+
+
+@pytest.mark.timeout(600)
+def test_rccl_world1_collectives(tmp_path):
+    """Every RCCL call of the product, executed on the GPU: a world-size-1
+    "nccl" process group on cuda:0 (init_process_group with device_id, as
+    bench.py and distributed.init_from_env do) runs the bench's MAX timing
+    all-reduce on an fp64 GPU tensor, its stream-count SUM, an fp32 tensor
+    all-reduce, evaluate()'s metric all-reduce over the (single) user shard
+    and FedAvg.sync of HIP-trained parameters; the same calls on gloo give
+    the same results (world size 1: the identity, bitwise)."""
+    outs = {}
+    for be in ("nccl", "gloo"):
+        d = tmp_path / be
+        d.mkdir()
+        outs[be] = _run("collectives", d, world=1, backend=be)[0]
+        outs[be]["pre"] = np.load(d / "rank0_pre.npy")
+        outs[be]["post"] = np.load(d / "rank0_post.npy")
+    r, g = outs["nccl"], outs["gloo"]
+    assert r["backend"] == "nccl" and g["backend"] == "gloo"
+    assert r["max"] == g["max"] == 1.25 and r["sum"] == g["sum"] == 4096.0
+    assert r["all_reduce"] == g["all_reduce"] == [float(i) for i in range(6)]
+    assert r["eval_group"] == r["eval_plain"] == g["eval_group"]
+    assert r["synced"] == g["synced"] == [False, True]
+    for o in (r, g):   # the average over one client is the client's model, bitwise
+        assert np.array_equal(o["post"], o["pre"])
+    assert np.array_equal(r["post"], g["post"])   # same kernels, same batches, same result
+
+
+@pytest.mark.timeout(600)
+def test_bench_rccl_world1(tmp_path):
+    """bench.py's multi-rank path with RCCL, on one GPU: torch.distributed.run
+    with one process, backend "nccl" (--init-dist takes the process-group
+    branch at world size 1: init with device_id, barriers, the MAX timing
+    all-reduce and the stream-count SUM); one JSON line, every impression of
+    the sampled stream scored, logits equal to the run without a group."""
+    n = 8192
+    common = ["--stream", "--stream-impressions", str(n), "--no-extras", "--no-cpu-baseline", "--warmup", "1"]
+    port = _free_port()
+    one = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                          "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "1",
+                          "--init-dist", "--dist-backend", "nccl", *common,
+                          "--dump-logits", str(tmp_path / "rccl")],
+                         cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert one.returncode == 0, one.stderr[-3000:]
+    lines = [ln for ln in one.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, one.stdout[-3000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 1 and rec["value"] > 0
+    plain = subprocess.run([sys.executable, "-u", "bench.py", *common, "--dump-logits", str(tmp_path / "plain")],
+                           cwd=ROOT, capture_output=True, text=True, timeout=400)
+    assert plain.returncode == 0, plain.stderr[-3000:]
+    a, b = np.load(tmp_path / "rccl.rank0.npz"), np.load(tmp_path / "plain.rank0.npz")
+    assert np.array_equal(a["idx"], np.arange(n)) and np.array_equal(a["idx"], b["idx"])
+    assert np.array_equal(a["logits"].view(np.uint32), b["logits"].view(np.uint32))
