@@ -586,6 +586,10 @@ def main():
                              "products per fp32 product, so see issue_floor for the instruction-level "
                              "ceiling"}
     if floor is not None:
+        # the fraction against the peak of the instructions the kernel actually
+        # issues (its split GEMM's 16-bit products at 2.5 PF dense, the f32
+        # attention / pooling at 157.3 TF): how far it is from its own ceiling
+        roofline["frac_vs_issued_peak"] = round(floor / stage_ms[dom], 4)
         roofline["issue_floor"] = {
             "ms": round(floor, 4), "frac": round(floor / stage_ms[dom], 4),
             "basis": (f"additive GEMM {args.gemm} ({ {'x6': 6, 'f16x3': 3}.get(args.gemm)} 16-bit products "

@@ -53,7 +53,10 @@ extern "C" {
  *    forward workspaces hold the title buckets (*_workspace_size grew). */
 /* 6: nrms_set_thread_gemm_arith / _title_dedupe / _token_compaction
  *    (per-thread overrides of the process-wide switches). */
-#define NRMS_ABI_VERSION 6
+/* 7: host-side readers of the eval split files (nrms_behaviors_scan /
+ *    nrms_behaviors_parse / nrms_news_parse); nrms_forward's workspace holds
+ *    the UserEncoder dispatch order (nrms_forward_workspace_size grew). */
+#define NRMS_ABI_VERSION 7
 
 typedef enum {
   NRMS_OK = 0,
@@ -436,6 +439,42 @@ typedef struct {
 
 int32_t nrms_adam_step_multi(const nrms_adam_tensor_t* tensors, int32_t n, float lr, float beta1,
                              float beta2, float eps, int64_t step, hipStream_t stream);
+
+/* ---------------------------------------------------------------------------
+ * Host-side readers of the eval split (csrc/tsv_io.hip). HOST pointers, no
+ * stream: they replace the Python line loop of the reference's readers
+ * (src/evaluate.py:55-71 news_parsed.tsv, :133-157 behaviors.tsv) for the
+ * MIND id form ("N<digits>" without leading zeros). Any other form -- a '\r',
+ * a non-ASCII byte, a cell outside the plain form below -- returns
+ * NRMS_ERR_UNSUPPORTED and the caller reads the file on its general path
+ * (newsrecommendationsystem_amd/data.py), which also raises the reference's
+ * errors. Values equal the general path's wherever these accept the input.
+ *
+ * behaviors.tsv: non-empty lines of at least five tab-separated columns
+ * (impression id, user, time, history, impressions); impressions cell
+ * "N<id>-<label>" tokens separated by single spaces (labels <= 9 digits);
+ * history cell blank or "N<id>" tokens separated by single spaces (outer
+ * spaces ignored, as str.strip). nrms_behaviors_scan checks the bytes and
+ * writes upper bounds of the lines, candidate tokens and history ids into
+ * counts[3]; nrms_behaviors_parse takes those (or any) capacities[3] and
+ * fills, per line k: fields[10 k + 2 c], [.. + 1] = byte span of column c;
+ * the candidates' numeric ids and labels and their count per line; the
+ * history ids and their count; and hist_user[k] = the index of line k's
+ * history string among the distinct history strings in first-seen order (an
+ * empty field counts as " ", as the reference's fillna(' ')); counts[4] =
+ * lines, candidates, history ids, distinct histories. NRMS_ERR_WORKSPACE
+ * when a capacity is short. */
+int32_t nrms_behaviors_scan(const char* buf, int64_t len, int64_t* counts);
+int32_t nrms_behaviors_parse(const char* buf, int64_t len, const int64_t* capacity, int64_t* counts,
+                             int64_t* fields, int64_t* cand_num, int32_t* labels, int64_t* cand_count,
+                             int64_t* hist_num, int64_t* hist_count, int64_t* hist_user);
+/* news_parsed.tsv: a header naming "id" and "title" columns, then rows whose
+ * id is N<digits> and whose title is a list literal of exactly L ints
+ * ("[12, 7, 0, ...]"). Writes *n_rows, and for the first `capacity` rows the
+ * numeric id, the id's byte span [2] and the title [L]; NRMS_ERR_WORKSPACE
+ * when there are more rows than `capacity` (*n_rows says how many). */
+int32_t nrms_news_parse(const char* buf, int64_t len, int32_t L, int64_t* n_rows, int64_t* ids,
+                        int64_t* id_spans, int64_t* titles, int64_t capacity);
 
 #ifdef __cplusplus
 }

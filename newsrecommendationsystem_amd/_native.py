@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NRMS_LIB_PATH") or os.path.join(_PKG, "libnrms_hip.so")   # override: A/B builds
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
 NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32, NRMS_GEMM_SPLIT_F16X3 = 0, 1, 2
@@ -91,6 +91,10 @@ SIGNATURES = {
     "nrms_forward_timed": (_i32, [_p, _p, _i64, _i32, _i32, _i32, _p, _i64, _EW, _EW, _i32, _p, _p,
                                   _sz, _p, _p, _i32]),
     "nrms_forward_stage_name": (ctypes.c_char_p, [_i32]),
+    # host-side readers (HOST pointers)
+    "nrms_behaviors_scan": (_i32, [_p, _i64, _p]),
+    "nrms_behaviors_parse": (_i32, [_p, _i64, _p, _p, _p, _p, _p, _p, _p, _p, _p]),
+    "nrms_news_parse": (_i32, [_p, _i64, _i32, _p, _p, _p, _p, _i64]),
 }
 NRMS_FORWARD_STAGES = 5
 

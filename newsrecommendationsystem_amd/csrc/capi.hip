@@ -487,7 +487,7 @@ size_t nrms_forward_workspace_size(int64_t B, int32_t C, int32_t N, int32_t L, i
   const int64_t n_all = B * (C + N);
   return nrms_news_encode_workspace_size(n_all, L, V, D, proj_mode) +
          align_up((size_t)n_all * D * 4) + align_up((size_t)B * D * 4) +
-         nrms_user_encode_workspace_size(B, N, D) + align_up((size_t)B * N * 8);
+         nrms_user_encode_workspace_size(B, N, D) + align_up((size_t)B * N * 8) + align_up((size_t)B * 4);
 }
 
 namespace {
@@ -525,6 +525,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   float* uwap = cv.floats(fused_user_packed_b_floats());
   float* upack = cv.floats(proj_x6_pack_floats());
   int64_t* ulist = reinterpret_cast<int64_t*>(cv.floats((size_t)n_clk * 2));
+  int32_t* uorder = reinterpret_cast<int32_t*>(cv.floats((size_t)B));   // user dispatch order
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   auto rec = [&](int i) -> int32_t {
     if (ev && hipEventRecord(ev[i], stream) != hipSuccess) return launch_status();
@@ -610,7 +611,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   if (user_fused)
     st = launch_fused_user(uqkv, uld, B, N, user_w->w_add, user_w->b_add, user_w->q_add, uwap, user,
                            stream, (user_dedupe || user_compact) ? &pg_flags : nullptr, prepacked, user_dedupe,
-                           user_compact);
+                           user_compact, uorder);
   else
     st = encode_from_qkv(uqkv, uld, n_clk, nullptr, B, nullptr, B, N, user_w, uctx, uscores, user,
                          stream);

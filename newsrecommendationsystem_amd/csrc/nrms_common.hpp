@@ -249,11 +249,13 @@ bool fused_user_supported(int L, int D, int H, int Q);
 // of copied padding titles (see PaddingGroups) were not projected and are read
 // from row *rep. compact (L <= 64): each user is encoded on its distinct rows,
 // its padding positions collapsed into one row with their count
-// (user_fused.hip).
+// (user_fused.hip). order (optional, B int32 of workspace, with compact):
+// the users are dispatched longest compacted length first (NRMS_USER_LPT=0
+// in the environment: in user order).
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
                           hipStream_t s, const PaddingGroups* pg = nullptr, bool prepacked = false,
-                          bool copied = false, bool compact = false);
+                          bool copied = false, bool compact = false, int32_t* order = nullptr);
 // Process-wide switch (news_fused.hip): encode one all-padding title per
 // batch and broadcast its vector (nrms_set_title_dedupe; NRMS_DEDUPE=0 in the
 // environment turns it off).

@@ -38,6 +38,8 @@
 #include "nrms_common.hpp"
 #include "packs.hpp"
 
+#include <atomic>
+#include <cstdlib>
 #include <type_traits>
 
 namespace nrms {
@@ -95,11 +97,46 @@ __device__ __forceinline__ int ukpos(int k) {
 // row-list projection after dedupe); the padding row is then rep's, else the
 // user's own first padding position's.
 constexpr int UF_COPIED = 1, UF_COMPACT = 2;
+
+// Dispatch order of the users (with compaction): longest compacted length Le
+// first, so that the last workgroups dispatched are the short users (LPT:
+// one workgroup per user and per CU, 23 k to 61 k cycles per user by Le --
+// dispatched in user order, the makespan was set by long users started
+// last). One block per 1,024 users: an LDS histogram over Le and a
+// descending scan; users of equal Le in any order (a user's result does not
+// depend on when its workgroup runs).
+constexpr int UORD_T = 1024;
+__global__ __launch_bounds__(UORD_T) void user_order_kernel(const uint8_t* __restrict__ pad, int64_t B,
+                                                            int L_all, int32_t* __restrict__ order) {
+  __shared__ int cnt[65], base[65];
+  const int64_t u = (int64_t)blockIdx.x * UORD_T + threadIdx.x;
+  if (threadIdx.x < 65) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  int le = -1;
+  if (u < B) {
+    const uint8_t* p = pad + u * L_all;
+    int npad = 0;
+    for (int i = 0; i < L_all; ++i) npad += p[i] ? 1 : 0;
+    le = L_all - npad + (npad > 0 ? 1 : 0);
+    atomicAdd(&cnt[le], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int l = 64; l >= 0; --l) {
+      base[l] = acc;
+      acc += cnt[l];
+    }
+  }
+  __syncthreads();
+  if (u < B) order[(int64_t)blockIdx.x * UORD_T + atomicAdd(&base[le], 1)] = (int32_t)u;
+}
+
 template <int MODE, int LMAX, int NT>
 __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     const float* __restrict__ qkv, int64_t ldq, int L_all, const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
-    PaddingGroups pg, int uflags) {
+    PaddingGroups pg, int uflags, const int32_t* __restrict__ order) {
   static_assert(NT >= UH * LMAX, "one (head, query) task per thread");
   constexpr int NW = NT / 64;
   constexpr int NTPW = (UNT + NW - 1) / NW;            // N-tiles per wave
@@ -122,7 +159,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   // MODE 2: part | wts | [64] hold one max |ctx| per (head, query) thread
   // until the split; then [64] row exponents ea
   int32_t* rexp = reinterpret_cast<int32_t*>(wts + 128);
-  const int64_t s = blockIdx.x;
+  const int64_t s = order ? (int64_t)order[blockIdx.x] : (int64_t)blockIdx.x;   // (user_order_kernel)
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   // q|k|v row of position i (stride ldq floats); with pg, a position holding a
@@ -576,27 +613,33 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 template <int MODE, int LMAX, int NT>
 int32_t launch_user_inst(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
-                         PaddingGroups pg, int uflags) {
+                         PaddingGroups pg, int uflags, const int32_t* order) {
   const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64 + 2 * 64) * 4;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>), (int)lds);
   hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
-                     ldq, L, wap, b_add, q_add, out, pg, uflags);
+                     ldq, L, wap, b_add, q_add, out, pg, uflags, order);
   return launch_status();
 }
 
 template <int MODE>
 int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
-                         PaddingGroups pg, int uflags) {
-  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
-  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
-  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
-  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
+                         PaddingGroups pg, int uflags, const int32_t* order) {
+  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order);
+  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order);
+  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order);
+  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order);
 }
 
 }  // namespace
 
 size_t fused_user_packed_b_floats() { return (size_t)UWAP_MAX + USTAMP_FLOATS; }
+
+static std::atomic<int> g_user_lpt{[] {
+  const char* e = getenv("NRMS_USER_LPT");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
+int set_user_lpt(int on) { return g_user_lpt.exchange(on ? 1 : 0); }
 
 bool fused_user_supported(int L, int D, int H, int Q) {
   return L >= 1 && L <= 64 && D == UD && H == UH && Q == UQ;
@@ -604,7 +647,8 @@ bool fused_user_supported(int L, int D, int H, int Q) {
 
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
-                          hipStream_t s, const PaddingGroups* pgp, bool prepacked, bool copied, bool compact) {
+                          hipStream_t s, const PaddingGroups* pgp, bool prepacked, bool copied, bool compact,
+                          int32_t* order) {
   const PaddingGroups pg = pgp ? *pgp : PaddingGroups{nullptr, nullptr, nullptr};
   if (compact && (!pgp || L > 64 || B * L > INT32_MAX)) return NRMS_ERR_UNSUPPORTED;
   if (copied && !pgp) return NRMS_ERR_INVALID_ARG;
@@ -620,9 +664,17 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
     hipLaunchKernelGGL(pack_user_b_kernel, dim3(blocks), dim3(256), 0, s, w_add, wap, mode);
     if (int32_t st = launch_status()) return st;
   }
-  if (mode == 2) return launch_user_mode<2>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
-  if (mode == 1) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
-  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags);
+  // longest users first (compaction only: Le comes from the padding flags)
+  const int32_t* ord = nullptr;
+  if (compact && order && g_user_lpt.load(std::memory_order_relaxed)) {
+    hipLaunchKernelGGL(user_order_kernel, dim3((unsigned)((B + UORD_T - 1) / UORD_T)), dim3(UORD_T), 0, s,
+                       pg.pad_title, B, L, order);
+    if (int32_t st = launch_status()) return st;
+    ord = order;
+  }
+  if (mode == 2) return launch_user_mode<2>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord);
+  if (mode == 1) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord);
+  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord);
 }
 
 }  // namespace nrms

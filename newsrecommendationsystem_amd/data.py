@@ -30,11 +30,15 @@ PADDED_NEWS = "PADDED_NEWS"
 # ---------------------------------------------------------------- readers
 class NewsCorpus:
     """news_parsed.tsv: ids (str), titles int64 [n, L]; id -> first row (the
-    reference keeps the first vector per id, src/evaluate.py:197-201)."""
+    reference keeps the first vector per id, src/evaluate.py:197-201).
+    `numeric` (optional): the ids' numbers when every id is "N<digits>"
+    without a leading zero (the native reader's parse; numeric_news_index
+    then skips its string pass)."""
 
-    def __init__(self, ids, titles):
+    def __init__(self, ids, titles, numeric=None):
         self.ids = list(ids)
         self.titles = np.ascontiguousarray(titles, dtype=np.int64)
+        self.numeric = numeric
         self.index = {}
         for i, nid in enumerate(self.ids):
             self.index.setdefault(nid, i)
@@ -64,7 +68,46 @@ def _parse_titles(cells, ids, num_words_title):
     return np.array(titles, dtype=np.int64).reshape(-1, num_words_title)
 
 
+def _read_bytes(path):
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def read_news_parsed_native(path, num_words_title=NUM_WORDS_TITLE):
+    """news_parsed.tsv through the native reader (nrms_news_parse: one C++ pass
+    over the bytes), or None when the file is not in its plain MIND form (the
+    caller then reads it with read_news_parsed's general path)."""
+    import ctypes
+    from . import _native as N
+    buf = _read_bytes(path)
+    cap = buf.count(b"\n") + 1
+    ids = np.empty(cap, np.int64)
+    spans = np.empty((cap, 2), np.int64)
+    titles = np.empty((cap, num_words_title), np.int64)
+    n = ctypes.c_int64(0)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    st = N.load().nrms_news_parse(buf, len(buf), num_words_title, ctypes.byref(n), P(ids), P(spans),
+                                  P(titles), cap)
+    if st == N.NRMS_ERR_UNSUPPORTED:
+        return None
+    N.check(st, "nrms_news_parse")
+    n = n.value
+    text = buf.decode("ascii")
+    names = [text[a:b] for a, b in spans[:n].tolist()]
+    return NewsCorpus(names, titles[:n], numeric=ids[:n].copy())
+
+
 def read_news_parsed(path, num_words_title=NUM_WORDS_TITLE):
+    """news_parsed.tsv -> NewsCorpus: the native reader for the plain MIND
+    form, else the csv module + _parse_titles (every form the reference's
+    pandas reader takes as a plain tab-separated table)."""
+    fast = read_news_parsed_native(path, num_words_title)
+    if fast is not None:
+        return fast
+    return read_news_parsed_py(path, num_words_title)
+
+
+def read_news_parsed_py(path, num_words_title=NUM_WORDS_TITLE):
     ids, cells = [], []
     with open(path, newline="") as f:
         rd = csv.reader(f, delimiter="\t", quoting=csv.QUOTE_NONE)
@@ -117,9 +160,111 @@ class Impression:
 
     @labels.setter
     def labels(self, v):
-        if self._cands is None:
+        if self._cands is None and self.raw is not None:
             self._parse()
         self._labels, self.raw = v, None
+
+
+class BehaviorsTable:
+    """A behaviors.tsv split parsed by the native reader (nrms_behaviors_parse)
+    into flat arrays: per impression the candidates' numeric ids, labels and
+    counts, the history ids, and the index of its history string among the
+    split's distinct histories (first-seen order). Indexing or iterating
+    yields Impression objects built from the raw columns, as read_behaviors
+    would; slicing and select() give sub-tables (EvalPlan's max_count
+    truncation, the user sharding)."""
+
+    def __init__(self, text, fields, cand_num, labels, cand_count, hist_num, hist_count, hist_user):
+        self.text = text
+        self.fields = fields                  # [n, 5, 2] byte spans of the columns
+        self.cand_num, self.labels, self.cand_count = cand_num, labels, cand_count
+        self.hist_num, self.hist_count = hist_num, hist_count
+        self.hist_user = hist_user            # distinct-history index (first-seen order)
+        self.cand_off = np.concatenate([[0], np.cumsum(cand_count)]).astype(np.int64)
+        self.hist_off = np.concatenate([[0], np.cumsum(hist_count)]).astype(np.int64)
+
+    def __len__(self):
+        return self.fields.shape[0]
+
+    def _col(self, k, c):
+        a, b = self.fields[k, c]
+        return self.text[a:b]
+
+    def _impression(self, k):
+        hist = self._col(k, 3)
+        return Impression(self._col(k, 0), self._col(k, 1), self._col(k, 2), hist if hist != "" else " ",
+                          raw=self._col(k, 4))
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            return self.select(np.arange(len(self))[k])
+        return self._impression(int(k))
+
+    def __iter__(self):
+        return (self._impression(k) for k in range(len(self)))
+
+    def users(self):
+        """The user column of every impression (str)."""
+        return [self.text[a:b] for a, b in self.fields[:, 1].tolist()]
+
+    def select(self, rows):
+        """Sub-table of the impressions `rows` (increasing), history indices
+        renumbered in first-seen order."""
+        rows = np.asarray(rows, dtype=np.int64)
+        cs = _ranges(self.cand_off[rows], self.cand_count[rows])
+        hs = _ranges(self.hist_off[rows], self.hist_count[rows])
+        _, first, inv = np.unique(self.hist_user[rows], return_index=True, return_inverse=True)
+        rank = np.empty(first.size, np.int64)
+        rank[np.argsort(first, kind="stable")] = np.arange(first.size)
+        return BehaviorsTable(self.text, self.fields[rows], self.cand_num[cs], self.labels[cs],
+                              self.cand_count[rows], self.hist_num[hs], self.hist_count[rows],
+                              rank[inv.reshape(-1)])
+
+
+def _ranges(starts, counts):
+    """Concatenated aranges [s, s + c) (int64)."""
+    counts = np.asarray(counts, np.int64)
+    tot = int(counts.sum())
+    if tot == 0:
+        return np.zeros(0, np.int64)
+    off = np.cumsum(counts) - counts
+    return np.repeat(np.asarray(starts, np.int64) - off, counts) + np.arange(tot)
+
+
+def read_behaviors_native(path):
+    """behaviors.tsv through the native reader (nrms_behaviors_scan /
+    _parse: one C++ pass over the bytes) as a BehaviorsTable, or None when the
+    file is not in the plain MIND form (read_behaviors' general path)."""
+    import ctypes
+    from . import _native as N
+    lib = N.load()
+    buf = _read_bytes(path)
+    P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+    cap = np.zeros(3, np.int64)
+    st = lib.nrms_behaviors_scan(buf, len(buf), P(cap))
+    if st == N.NRMS_ERR_UNSUPPORTED:
+        return None
+    N.check(st, "nrms_behaviors_scan")
+    n, nc, nh = (int(x) for x in cap)
+    fields = np.empty((n, 5, 2), np.int64)
+    cand_num, labels, cand_count = np.empty(nc, np.int64), np.empty(nc, np.int32), np.empty(n, np.int64)
+    hist_num, hist_count, hist_user = np.empty(nh, np.int64), np.empty(n, np.int64), np.empty(n, np.int64)
+    counts = np.zeros(4, np.int64)
+    st = lib.nrms_behaviors_parse(buf, len(buf), P(cap), P(counts), P(fields), P(cand_num), P(labels),
+                                  P(cand_count), P(hist_num), P(hist_count), P(hist_user))
+    if st == N.NRMS_ERR_UNSUPPORTED:
+        return None
+    N.check(st, "nrms_behaviors_parse")
+    n, nc, nh = (int(x) for x in counts[:3])
+    return BehaviorsTable(buf.decode("ascii"), fields[:n], cand_num[:nc], labels[:nc], cand_count[:n],
+                          hist_num[:nh], hist_count[:n], hist_user[:n])
+
+
+def load_behaviors(path):
+    """behaviors.tsv as evaluate() reads it: a BehaviorsTable from the native
+    reader for the plain MIND form, else read_behaviors' list of Impression."""
+    tab = read_behaviors_native(path)
+    return tab if tab is not None else read_behaviors(path)
 
 
 def read_behaviors(path):
@@ -152,15 +297,17 @@ def numeric_news_index(corpus):
     if not ids:
         return None
     n = len(ids)
-    if max(map(len, ids)) > 19:
-        return None
-    joined = " ".join(ids)
-    if (joined.translate(_DIGITS) != " ".join(["N"] * n) or joined.count("N0") != joined.count("N0 ") + (
-            1 if joined.endswith("N0") else 0)):
-        return None
-    nums = np.fromstring(joined.replace("N", " "), dtype=np.int64, sep=" ")
-    if nums.size != n:
-        return None
+    nums = getattr(corpus, "numeric", None)
+    if nums is None:
+        if max(map(len, ids)) > 19:
+            return None
+        joined = " ".join(ids)
+        if (joined.translate(_DIGITS) != " ".join(["N"] * n) or joined.count("N0") != joined.count("N0 ") + (
+                1 if joined.endswith("N0") else 0)):
+            return None
+        nums = np.fromstring(joined.replace("N", " "), dtype=np.int64, sep=" ")
+        if nums.size != n:
+            return None
     uniq, first = np.unique(nums, return_index=True)   # (the first row of a repeated id)
     if int(uniq[-1]) > 16 * n + (1 << 20):
         return None

@@ -30,7 +30,15 @@ def user_rank(user, world):
 
 
 def shard_impressions(impressions, rank, world):
-    """The impressions whose user this rank owns, in their original order."""
+    """The impressions whose user this rank owns, in their original order (a
+    data.BehaviorsTable stays a table)."""
+    from .data import BehaviorsTable
+    if isinstance(impressions, BehaviorsTable):
+        if world <= 1:
+            return impressions
+        import numpy as np
+        mine = np.array([user_rank(u, world) == rank for u in impressions.users()], dtype=bool)
+        return impressions.select(np.flatnonzero(mine))
     if world <= 1:
         return list(impressions)
     return [im for im in impressions if user_rank(im.user, world) == rank]

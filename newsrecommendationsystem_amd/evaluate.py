@@ -24,8 +24,9 @@ import numpy as np
 import torch
 
 from . import _native as N
-from .data import (PADDED_NEWS, candidate_rows_numeric, history_ids, history_rows_numeric, numeric_news_index,
-                   parse_impression_cells, read_behaviors, read_news_parsed)
+from .data import (PADDED_NEWS, BehaviorsTable, _index_rows, candidate_rows_numeric, history_ids,
+                   history_rows_numeric, load_behaviors, numeric_news_index, parse_impression_cells,
+                   read_news_parsed)
 
 
 class EvalPlan:
@@ -41,9 +42,17 @@ class EvalPlan:
         # the reference breaks when count == max_count before scoring it
         # (src/evaluate.py:245-249): impressions 1..max_count-1 are scored
         n = len(impressions) if max_count > len(impressions) else max(0, max_count - 1)
-        self.impressions = impressions[:n]
         self.corpus = corpus
+        self.num_clicked = num_clicked
         pad = len(corpus)
+        if isinstance(impressions, BehaviorsTable):
+            tab = impressions if n == len(impressions) else impressions[:n]
+            nindex = numeric_news_index(corpus)
+            if nindex is not None:
+                self._from_table(tab, nindex, num_clicked, pad)
+                return
+            impressions = list(tab)   # (ids not in the numeric form: the per-name path)
+        self.impressions = impressions[:n]
         # users keyed by history string, in first-seen order
         hist_of = {}
         hists = []
@@ -79,7 +88,29 @@ class EvalPlan:
                 rows[real] = lookup([x for x, r in zip(hist_names, real) if r])
             hrows = rows.reshape(len(hists), num_clicked)
         self.hist_rows = hrows
-        self.num_clicked = num_clicked
+
+    def _from_table(self, tab, nindex, num_clicked, pad):
+        """The plan from a natively parsed split (data.BehaviorsTable): the
+        same arrays as the Impression path's numeric fast path."""
+        self.impressions = tab
+        n = len(tab)
+        self.cand = _index_rows(nindex, tab.cand_num)
+        self.labels = tab.labels
+        counts = tab.cand_count
+        imp_user = tab.hist_user
+        self.pair_user = np.repeat(imp_user, counts)
+        self.offsets = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        # each distinct history's first line: its first num_clicked ids, left-padded
+        _, first = np.unique(imp_user, return_index=True) if n else (None, np.zeros(0, np.int64))
+        U = first.size
+        hc, ho = tab.hist_count[first], tab.hist_off[first]
+        m = np.minimum(hc, num_clicked)
+        rows = np.full((U, num_clicked), pad, dtype=np.int64)
+        if int(m.sum()):
+            u = np.repeat(np.arange(U), m)
+            k = np.arange(int(m.sum())) - np.repeat(np.cumsum(m) - m, m)
+            rows[u, num_clicked - np.repeat(m, m) + k] = _index_rows(nindex, tab.hist_num[np.repeat(ho, m) + k])
+        self.hist_rows = rows
 
     @property
     def n_impressions(self):
@@ -164,7 +195,7 @@ def evaluate(model, directory, num_workers=4, max_count=sys.maxsize, process_gro
     (distributed.user_rank: user_id % world) and the metric sums are all-reduced."""
     import os
     corpus = read_news_parsed(os.path.join(directory, "news_parsed.tsv"))
-    imps = read_behaviors(os.path.join(directory, "behaviors.tsv"))
+    imps = load_behaviors(os.path.join(directory, "behaviors.tsv"))
     return evaluate_split(model, corpus, imps, max_count, process_group)
 
 

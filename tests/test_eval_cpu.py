@@ -208,3 +208,70 @@ def test_impression_setters_keep_the_other_field():
     im.labels = [0, 0]
     assert im.candidates == ["N1", "N2"] and im.labels == [0, 0]
 
+
+
+# ---------------------------------------------------------------- native readers (csrc/tsv_io.hip)
+def _write(path, text):
+    with open(path, "w", newline="") as f:
+        f.write(text)
+
+
+def test_native_readers_equal_python_readers(split):
+    """nrms_news_parse / nrms_behaviors_parse (host C++, ABI 7) give the
+    corpus, the impressions' columns and the EvalPlan arrays of the Python
+    readers (data.read_news_parsed_py, read_behaviors + the numeric fast path,
+    themselves pinned to the reference's per-token split / literal_eval)."""
+    d, _, _ = split
+    nat = Dt.read_news_parsed_native(d + "/news_parsed.tsv")
+    py = Dt.read_news_parsed_py(d + "/news_parsed.tsv")
+    assert nat is not None and nat.ids == py.ids and np.array_equal(nat.titles, py.titles)
+    assert np.array_equal(Dt.numeric_news_index(nat), Dt.numeric_news_index(py))
+    tab = Dt.read_behaviors_native(d + "/behaviors.tsv")
+    imps = Dt.read_behaviors(d + "/behaviors.tsv")
+    assert isinstance(tab, Dt.BehaviorsTable) and len(tab) == len(imps)
+    for a, b in zip(tab, imps):
+        assert (a.impression_id, a.user, a.time, a.clicked_news, a.raw) == \
+               (b.impression_id, b.user, b.time, b.clicked_news, b.raw)
+    for mc in (sys.maxsize, 1, 2, 7):
+        p1, p2 = EvalPlan(nat, tab, max_count=mc), EvalPlan(py, imps, max_count=mc)
+        for k in ("cand", "labels", "pair_user", "offsets", "hist_rows"):
+            a, b = getattr(p1, k), getattr(p2, k)
+            assert a.dtype == b.dtype and np.array_equal(a, b), (mc, k)
+
+
+def test_native_behaviors_edge_forms(tmp_path):
+    """Blank and space-padded histories, a repeated history string, "N0",
+    multi-digit labels, fewer lines than the scan's bound: the native table
+    equals the Python reader; non-plain forms (CRLF, double spaces, a leading
+    zero, a missing column, non-ASCII) return None so the general path runs."""
+    corpus = Dt.NewsCorpus([f"N{i}" for i in range(12)], np.arange(240).reshape(12, 20))
+    text = ("1\tU1\tt\t\tN3-1 N0-0\n"
+            "2\tU2\tt\t N1 N2 \tN5-01 N6-0\n\n"
+            "3\tU1\tt\t\tN7-1\n"
+            "4\tU9\tt\tN1 N2\tN11-0 N10-1 N9-0\textra\n")
+    p = str(tmp_path / "b.tsv")
+    _write(p, text)
+    tab = Dt.read_behaviors_native(p)
+    imps = Dt.read_behaviors(p)
+    assert tab is not None and len(tab) == 4
+    assert [im.clicked_news for im in tab] == [im.clicked_news for im in imps] == [" ", " N1 N2 ", " ", "N1 N2"]
+    assert tab.hist_user.tolist() == [0, 1, 0, 2]
+    p1, p2 = EvalPlan(corpus, tab, num_clicked=3), EvalPlan(corpus, imps, num_clicked=3)
+    for k in ("cand", "labels", "pair_user", "offsets", "hist_rows"):
+        assert np.array_equal(getattr(p1, k), getattr(p2, k)), k
+    assert p1.labels.tolist() == [1, 0, 1, 0, 1, 0, 1, 0]
+    shard = Dt.BehaviorsTable.select(tab, [1, 3])
+    assert [im.impression_id for im in shard] == ["2", "4"] and shard.hist_user.tolist() == [0, 1]
+    for bad in ("1\tU1\tt\tN1\tN3-1\r\n", "1\tU1\tt\tN1  N2\tN3-1\n", "1\tU1\tt\tN01\tN3-1\n",
+                "1\tU1\tt\tN1\tN3-1  N4-0\n", "1\tU1\tt\tN1\n", "1\tU1\tt\tN1\tN3-1 \n", "1\tUé\tt\tN1\tN3-1\n",
+                "1\tU1\tt\tN1\tN3-\n", "1\tU1\tt\tN1\tN03-1\n"):
+        _write(p, bad)
+        assert Dt.read_behaviors_native(p) is None, repr(bad)
+    n = str(tmp_path / "n.tsv")
+    _write(n, "id\tcategory\ttitle\nN1\tx\t[1, 2]\nN2\ty\t[3,4]\n")
+    c = Dt.read_news_parsed_native(n, num_words_title=2)
+    assert c.ids == ["N1", "N2"] and c.titles.tolist() == [[1, 2], [3, 4]] and c.numeric.tolist() == [1, 2]
+    for bad in ("id\ttitle\nN1\t[1, 2, 3]\n", "id\ttitle\nN01\t[1, 2]\n", "id\ttitle\nX1\t[1, 2]\n",
+                "id\ttitle\nN1\t(1, 2)\n", "idx\ttitle\nN1\t[1, 2]\n", "id\ttitle\r\nN1\t[1, 2]\r\n"):
+        _write(n, bad)
+        assert Dt.read_news_parsed_native(n, num_words_title=2) is None, repr(bad)
