@@ -424,6 +424,15 @@ struct QkvOffsets {
   __device__ static int v4(int g, int hl, int x) { return 608 + FDK * (4 * g + hl) + 5 * x; }
   __device__ static int v1(int g, int hl, int x) { return 608 + FDK * (4 * g + hl) + 5 * x + 4; }
 };
+#elif defined(NRMS_VPERM)
+// (probe) V dims of each head stored as [0-3 | 5-8 | 10-13 | 15-18 | 4 9 14 19]:
+// lane x's four dims 5x..5x+3 one aligned 16-B load, dim 5x+4 a 4-B load
+struct QkvOffsets {
+  __device__ static int q(int g, int hl, int c) { return FDK * (4 * g + hl) + 4 * c; }
+  __device__ static int k(int g, int hl, int c) { return FD + FDK * (4 * g + hl) + 4 * c; }
+  __device__ static int v4(int g, int hl, int x) { return 2 * FD + FDK * (4 * g + hl) + 4 * x; }
+  __device__ static int v1(int g, int hl, int x) { return 2 * FD + FDK * (4 * g + hl) + 16 + x; }
+};
 #else
 struct QkvOffsets {
   __device__ static int q(int g, int hl, int c) { return FDK * (4 * g + hl) + 4 * c; }
@@ -752,6 +761,16 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #endif
 
   int it = 0;
+#ifdef NRMS_W0_EARLY
+  // (probe) the first k-step's W_add fragments (H3) loaded at the end of phase
+  // A, before the A -> B barrier: the barrier wait covers their L2 latency
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(WaP + WAP_MAX + SPECIAL_FLOATS), 0, WAP2_FLOATS * 4, 0x00020000);
+  int wvoff[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) wvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
+  f16x8 wb0[4][3];
+#endif
   // one iteration: group key_at(idx), of bucket NB - 1
   auto iterate = [&](int64_t idx, auto nbc) {
     constexpr int NB = decltype(nbc)::value;
@@ -900,6 +919,15 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           if (i == 0) r_next = stage2(s_next, c_next);
         }
         stage3(s_next, r_next, c_next, nbuf);
+#ifdef NRMS_W0_EARLY
+        if constexpr (H3) {
+#pragma unroll
+          for (int pl = 2; pl >= 1; --pl)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              wb0[j][pl] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[j], pl * 1024, 0));
+        }
+#endif
       }
       NRMS_STAMP(1)
       __syncthreads();   // context tile complete
@@ -1024,8 +1052,54 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
             NRMS_H3STEP(1, 2) NRMS_H3STEP(0, 1) NRMS_H3STEP(0, 0)
 #undef NRMS_H3STEP
           };
+#define NRMS_H3STEP2(PA, PB)                                                                           \
+  _Pragma("unroll") for (int mt = 0; mt < NB; ++mt)                                                    \
+  _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                        \
+      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);  \
+  accX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ax[PA], bb[3][PB], accX, 0, 0, 0);                     \
+  if (extra) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
           f16x8 b0[4][3], b1[4][3];
+#ifdef NRMS_W0_EARLY
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { b0[j][1] = wb0[j][1]; b0[j][2] = wb0[j][2]; }
+#else
           load_b(0, b0);
+#endif
+#ifdef NRMS_AFRAG_DB
+          // (probe) the A fragments of k-step ks + 1 read from LDS during k-step
+          // ks's MFMAs (two register buffers): the LDS latency leaves the k-step
+          auto load_a = [&](int ks, f16x8 (&a)[NB][2], f16x8 (&ax)[2]) {
+#pragma unroll
+            for (int pl = 1; pl >= 0; --pl) {
+#pragma unroll
+              for (int mt = 0; mt < NB; ++mt)
+                a[mt][pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * mt * XRH + pl * XKP + 32 * ks);
+              ax[pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * xm * XRH + pl * XKP + 32 * ks);
+            }
+          };
+          auto kstep2 = [&](f16x8 (&bb)[4][3], const f16x8 (&a)[NB][2], const f16x8 (&ax)[2]) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bb[j][0] = bb[j][2] * (_Float16)kF16LoScale;
+            NRMS_H3STEP2(1, 2) NRMS_H3STEP2(0, 1) NRMS_H3STEP2(0, 0)
+          };
+          f16x8 aa0[NB][2], aax0[2], aa1[NB][2], aax1[2];
+          load_a(0, aa0, aax0);
+#pragma unroll
+          for (int ks = 0; ks < XKS; ks += 2) {
+            load_b(ks + 1, b1);
+            load_a(ks + 1, aa1, aax1);
+            __builtin_amdgcn_sched_barrier(0);
+            kstep2(b0, aa0, aax0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + 2 < XKS) {
+              load_b(ks + 2, b0);
+              load_a(ks + 2, aa0, aax0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            kstep2(b1, aa1, aax1);
+            __builtin_amdgcn_sched_barrier(0);
+          }
+#else
           // fully unrolled, each k-step's loads and MFMAs fenced in place
           // (without the fences the scheduler hoists every load: 1,100 spills);
           // a rolled loop permuted the accumulators at its back-edge (~170
@@ -1045,6 +1119,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
             kstep(ks + 1, b1);
             __builtin_amdgcn_sched_barrier(0);
           }
+#endif
           // (the 2^-11 unscale is folded into the epilogue's exp argument)
         } else {
           float4 bb[4], bn4[4];

@@ -1,0 +1,25 @@
+"""Config 5's quality half at the reference's dimensions (quality.run_scaled;
+src/train.py:161-236 then src/evaluate.py:171-272): two FedAvg clients x 320
+local steps of batch 128 at V = 70,976 on a planted-teacher corpus, the HIP
+student (HIP training kernels + HipAdam) against the reference student (the
+reference's op sequence on ATen autograd + torch.optim.Adam, on the GPU as
+src/train.py:24 selects), both from one initialisation on the same batches;
+with dropout 0 and with dropout 0.2 (the HIP masks fed to the reference
+path). MIND is absent, so the planted teacher stands in for MIND-small dev
+(SURVEY §8d): parity unpinned by MIND itself, pinned to the reference op
+sequence run on the same batches."""
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.timeout(600)
+def test_fedavg_quality_reference_scale():
+    from newsrecommendationsystem_amd import quality as Q
+    res = Q.run_scaled()
+    assert [r["dropout"] for r in res["runs"]] == [0.0, 0.2]
+    for r in res["runs"]:
+        assert r["abs_diff_auc"] <= 0.002, r
+        assert r["auc_lift_hip"] >= 0.04, r          # training moved the student (0.050 / 0.044 measured)
+        assert abs(r["auc_reference"] - r["auc_init"]) >= 0.04, r
+        assert r["max_normwise_param_diff_excl_WK_bias"] < 5e-3, r
