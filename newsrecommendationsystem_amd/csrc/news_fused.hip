@@ -58,10 +58,13 @@ constexpr int WAP_FLOATS = FKG * FNT * 64 * 4;             // packed Wa
 constexpr int ROW = (3 * FD + 31) / 32 * 32;               // zero / NaN row slots (928 floats: room for any q|k|v offset)
 constexpr int SPECIAL_FLOATS = 2 * ROW;                    // zero row + NaN row
 // after the context tile: row partials [80][PART_STRIDE] (the four waves' N-tile
-// sums + the N-tile-12 sum), row pointers [2][80] (u64), title meta [2][8] and
-// the group schedule [16] (int32)
+// sums + the N-tile-12 sum), row pointers [RPB][80] (u64), title meta [RPB][8]
+// and the group schedule [16] (int32). RPB buffers: a group's row pointers are
+// written two groups ahead (its Q slices load during the previous group's
+// attention), and a buffer is rewritten only after a barrier past its readers.
 constexpr int PART_STRIDE = 8;
-constexpr int TAIL_FLOATS = PART_STRIDE * FROWS + 2 * 2 * FROWS + 16 + 16;
+constexpr int RPB = 4;
+constexpr int TAIL_FLOATS = PART_STRIDE * FROWS + 2 * RPB * FROWS + 8 * RPB + 16;
 constexpr int LDS_FLOATS = FROWS * SC + TAIL_FLOATS;   // ctx, partials, rowptr, meta
 constexpr size_t LDS_BYTES = LDS_FLOATS * sizeof(float);
 
@@ -424,15 +427,6 @@ struct QkvOffsets {
   __device__ static int v4(int g, int hl, int x) { return 608 + FDK * (4 * g + hl) + 5 * x; }
   __device__ static int v1(int g, int hl, int x) { return 608 + FDK * (4 * g + hl) + 5 * x + 4; }
 };
-#elif defined(NRMS_VPERM)
-// (probe) V dims of each head stored as [0-3 | 5-8 | 10-13 | 15-18 | 4 9 14 19]:
-// lane x's four dims 5x..5x+3 one aligned 16-B load, dim 5x+4 a 4-B load
-struct QkvOffsets {
-  __device__ static int q(int g, int hl, int c) { return FDK * (4 * g + hl) + 4 * c; }
-  __device__ static int k(int g, int hl, int c) { return FD + FDK * (4 * g + hl) + 4 * c; }
-  __device__ static int v4(int g, int hl, int x) { return 2 * FD + FDK * (4 * g + hl) + 4 * x; }
-  __device__ static int v1(int g, int hl, int x) { return 2 * FD + FDK * (4 * g + hl) + 16 + x; }
-};
 #else
 struct QkvOffsets {
   __device__ static int q(int g, int hl, int c) { return FDK * (4 * g + hl) + 4 * c; }
@@ -530,9 +524,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   __bf16* ctxB = reinterpret_cast<__bf16*>(lds);       // x6:  [80][XRB] = hi | mid | lo planes
   _Float16* ctxH = reinterpret_cast<_Float16*>(lds);   // f16x3: [80][XRH] = hi | lo planes
   float* part = X6 ? lds + FROWS * XRB / 2 : (H3 ? lds + FROWS * XRH / 2 : ctxL + FROWS * SC);   // [80][8] row partials
-  const float** rowptr = reinterpret_cast<const float**>(part + PART_STRIDE * FROWS);   // [2][4 titles][20 slots]
-  int32_t* tmeta = reinterpret_cast<int32_t*>(rowptr + 2 * FROWS);   // [2][title index x4 | count x4]
-  int32_t* sched = tmeta + 16;   // [gend x NBK | bucket counts x NBK | rep | groups] (see below)
+  const float** rowptr = reinterpret_cast<const float**>(part + PART_STRIDE * FROWS);   // [RPB][4 titles][20 slots]
+  int32_t* tmeta = reinterpret_cast<int32_t*>(rowptr + RPB * FROWS);   // [RPB][title index x4 | count x4]
+  int32_t* sched = tmeta + 8 * RPB;   // [gend x NBK | bucket counts x NBK | rep | groups] (see below)
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float* zero_row = WaP + WAP_MAX;
@@ -696,15 +690,27 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   // at the start of the B epilogue (in flight behind the tanh work, a barrier
   // and the pooling), V at the end of C (behind the next S^T phase).
   float qf[5][FDK], kf[5][FDK], vf[FL][5];
-  auto prefetch_qk_tok = [&](int buf, int j) {   // token x + 4j of the lane's title
+  // token x + 4j of the lane's title: its Q slice (loaded in the previous
+  // group's attention as query column j retires) and K slice (B epilogue)
+  auto prefetch_q_tok = [&](int buf, int j) {
     const float* rp = rowptr[buf * FROWS + FL * at + x + 4 * j];
 #pragma unroll
     for (int c = 0; c < FDK / 4; ++c) {
       const floatx4 a = *gptr<floatx4>(rp + Off::q(w, hls, c));
-      const floatx4 b = *gptr<floatx4>(rp + Off::k(w, hls, c));
       qf[j][4 * c] = a.x; qf[j][4 * c + 1] = a.y; qf[j][4 * c + 2] = a.z; qf[j][4 * c + 3] = a.w;
+    }
+  };
+  auto prefetch_k_tok = [&](int buf, int j) {
+    const float* rp = rowptr[buf * FROWS + FL * at + x + 4 * j];
+#pragma unroll
+    for (int c = 0; c < FDK / 4; ++c) {
+      const floatx4 b = *gptr<floatx4>(rp + Off::k(w, hls, c));
       kf[j][4 * c] = b.x; kf[j][4 * c + 1] = b.y; kf[j][4 * c + 2] = b.z; kf[j][4 * c + 3] = b.w;
     }
+  };
+  auto prefetch_qk_tok = [&](int buf, int j) {
+    prefetch_q_tok(buf, j);
+    prefetch_k_tok(buf, j);
   };
   // slices past the next group's rows are zeroed, not left alone: a register
   // the next group might read is live across the GEMM otherwise (spills)
@@ -741,14 +747,29 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     }
   };
 
+  // the row pointers of the first two groups (buffers 0 and 1), the title
+  // indices of the third (s_carry), then the first group's slices
+  int32_t s_carry = -1;
   {
-    int tm0;
-    int64_t g0 = 0;
-    const int b0 = (int64_t)blockIdx.x < n_iter ? bucket_of(key_at(blockIdx.x, tm0), g0) : -1;
-    int c0;
-    const int32_t s0 = stage1(b0, g0);
-    const int64_t r0 = stage2(s0, c0);
-    stage3(s0, r0, c0, 0);
+    int b0 = -1;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      int tm0;
+      int64_t g0 = 0;
+      const int64_t i0 = (int64_t)blockIdx.x + (int64_t)p * gridDim.x;
+      const int b = i0 < n_iter ? bucket_of(key_at(i0, tm0), g0) : -1;
+      if (p == 0) b0 = b;
+      int c0;
+      const int32_t s0 = stage1(b, g0);
+      const int64_t r0 = stage2(s0, c0);
+      stage3(s0, r0, c0, p);
+    }
+    {
+      int tm2;
+      int64_t g2 = 0;
+      const int64_t i2 = (int64_t)blockIdx.x + 2 * (int64_t)gridDim.x;
+      s_carry = stage1(i2 < n_iter ? bucket_of(key_at(i2, tm2), g2) : -1, g2);
+    }
     __syncthreads();
     if (b0 >= 0) {
       prefetch_qk(0, b0 + 1);
@@ -761,16 +782,14 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #endif
 
   int it = 0;
-#ifdef NRMS_W0_EARLY
-  // (probe) the first k-step's W_add fragments (H3) loaded at the end of phase
-  // A, before the A -> B barrier: the barrier wait covers their L2 latency
+  // H3: the first k-step's W_add fragments are loaded at the end of phase A,
+  // before the A -> B barrier: the barrier wait covers their L2 latency
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
       const_cast<float*>(WaP + WAP_MAX + SPECIAL_FLOATS), 0, WAP2_FLOATS * 4, 0x00020000);
   int wvoff[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) wvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
   f16x8 wb0[4][3];
-#endif
   // one iteration: group key_at(idx), of bucket NB - 1
   auto iterate = [&](int64_t idx, auto nbc) {
     constexpr int NB = decltype(nbc)::value;
@@ -781,7 +800,15 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const int64_t kn = key_at(idx + gridDim.x, tmask_n);
     const int bn = (idx + gridDim.x < n_iter) ? bucket_of(kn, gn) : -1;
     const int nb_next = bn + 1;   // 0: no next group
-    const int buf = it & 1, nbuf = buf ^ 1;
+    // the group after next has its row pointers staged during this attention
+    // (its title indices were read at the end of the previous group: s_carry);
+    // the group after that has its title indices read at the end of this one
+    int tmask_n3;
+    int64_t gn3 = 0;
+    const int64_t kn3 = key_at(idx + 3 * (int64_t)gridDim.x, tmask_n3);
+    const int bn3 = (idx + 3 * (int64_t)gridDim.x < n_iter) ? bucket_of(kn3, gn3) : -1;
+    // row-pointer buffers: this group's, the next group's, the one after's
+    const int buf = it & (RPB - 1), nbuf = (it + 1) & (RPB - 1), nbuf2 = (it + 2) & (RPB - 1);
     {
       // this lane's title's real-token count (its index is read in C)
       const int my_c = tmeta[8 * buf + 4 + at];
@@ -806,7 +833,10 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         // the next group's slot rows (stage 1 now, stage 2 after the first
         // query column, stored at the end of this phase for the prefetch in
         // this group's B epilogue)
-        const int32_t s_next = stage1(bn, gn);
+        // (stage 1, the title index, came from the end of the previous group:
+        // its global load has landed, so stage 2's dependent row-id loads
+        // start at once and are done long before stage 3 at this phase's end)
+        const int32_t s_next = s_carry;
         int c_next = 0;
         int64_t r_next = -2;
         // S^T tiles: rows = keys 4j + r (A = K), cols = queries 4i + x (B = Q)
@@ -913,13 +943,16 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #pragma unroll
         for (int i = 0; i < NB; ++i) {
           s_mfma(i);
+          // query column i's Q slices are dead: the next group's go into them
+          // (main pass: the next group is of this bucket or a smaller one, so
+          // its queries are tokens < 4 NB; slots past its rows read the zero row)
+          if constexpr (!EXACT) prefetch_q_tok(nbuf, i);
           s_exp(i);
           o_mfma(i);
           o_store(i);
           if (i == 0) r_next = stage2(s_next, c_next);
         }
-        stage3(s_next, r_next, c_next, nbuf);
-#ifdef NRMS_W0_EARLY
+        stage3(s_next, r_next, c_next, nbuf2);
         if constexpr (H3) {
 #pragma unroll
           for (int pl = 2; pl >= 1; --pl)
@@ -927,7 +960,6 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
             for (int j = 0; j < 4; ++j)
               wb0[j][pl] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(wrs, wvoff[j], pl * 1024, 0));
         }
-#endif
       }
       NRMS_STAMP(1)
       __syncthreads();   // context tile complete
@@ -1031,95 +1063,61 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
                 dst[j][pl] = __builtin_bit_cast(f16x8, __builtin_amdgcn_raw_buffer_load_b128(
                     brs, bvoff[j], (ks * FNT * 3 + pl) * 1024, 0));
           };
-          // (one copy of the k-step for every wave, as the x6 path)
-          auto kstep = [&](int ks, f16x8 (&bb)[4][3]) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bb[j][0] = bb[j][2] * (_Float16)kF16LoScale;
-            f16x8 a[NB][2], ax[2];
-#pragma unroll
-            for (int pl = 1; pl >= 0; --pl) {
-#pragma unroll
-              for (int mt = 0; mt < NB; ++mt)
-                a[mt][pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * mt * XRH + pl * XKP + 32 * ks);
-              ax[pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * xm * XRH + pl * XKP + 32 * ks);
-            }
-#define NRMS_H3STEP(PA, PB)                                                                            \
-  _Pragma("unroll") for (int mt = 0; mt < NB; ++mt)                                                    \
-  _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                        \
-      acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);  \
-  accX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ax[PA], bb[3][PB], accX, 0, 0, 0);                     \
-  if (extra) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
-            NRMS_H3STEP(1, 2) NRMS_H3STEP(0, 1) NRMS_H3STEP(0, 0)
-#undef NRMS_H3STEP
-          };
+          // products lo·hi, hi·lo, hi·hi' of one k-step (one copy of the k-step
+          // for every wave, as the x6 path)
 #define NRMS_H3STEP2(PA, PB)                                                                           \
   _Pragma("unroll") for (int mt = 0; mt < NB; ++mt)                                                    \
   _Pragma("unroll") for (int j = 0; j < 3; ++j)                                                        \
       acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][PA], bb[j][PB], acc[mt][j], 0, 0, 0);  \
   accX = __builtin_amdgcn_mfma_f32_16x16x32_f16(ax[PA], bb[3][PB], accX, 0, 0, 0);                     \
   if (extra) accX2 = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[NB - 1][PA], bb[3][PB], accX2, 0, 0, 0);
-          f16x8 b0[4][3], b1[4][3];
-#ifdef NRMS_W0_EARLY
-#pragma unroll
-          for (int j = 0; j < 4; ++j) { b0[j][1] = wb0[j][1]; b0[j][2] = wb0[j][2]; }
-#else
-          load_b(0, b0);
-#endif
-#ifdef NRMS_AFRAG_DB
-          // (probe) the A fragments of k-step ks + 1 read from LDS during k-step
-          // ks's MFMAs (two register buffers): the LDS latency leaves the k-step
-          auto load_a = [&](int ks, f16x8 (&a)[NB][2], f16x8 (&ax)[2]) {
-#pragma unroll
-            for (int pl = 1; pl >= 0; --pl) {
-#pragma unroll
-              for (int mt = 0; mt < NB; ++mt)
-                a[mt][pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * mt * XRH + pl * XKP + 32 * ks);
-              ax[pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * xm * XRH + pl * XKP + 32 * ks);
-            }
-          };
-          auto kstep2 = [&](f16x8 (&bb)[4][3], const f16x8 (&a)[NB][2], const f16x8 (&ax)[2]) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) bb[j][0] = bb[j][2] * (_Float16)kF16LoScale;
-            NRMS_H3STEP2(1, 2) NRMS_H3STEP2(0, 1) NRMS_H3STEP2(0, 0)
-          };
-          f16x8 aa0[NB][2], aax0[2], aa1[NB][2], aax1[2];
-          load_a(0, aa0, aax0);
-#pragma unroll
-          for (int ks = 0; ks < XKS; ks += 2) {
-            load_b(ks + 1, b1);
-            load_a(ks + 1, aa1, aax1);
-            __builtin_amdgcn_sched_barrier(0);
-            kstep2(b0, aa0, aax0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (ks + 2 < XKS) {
-              load_b(ks + 2, b0);
-              load_a(ks + 2, aa0, aax0);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            kstep2(b1, aa1, aax1);
-            __builtin_amdgcn_sched_barrier(0);
-          }
-#else
           // fully unrolled, each k-step's loads and MFMAs fenced in place
           // (without the fences the scheduler hoists every load: 1,100 spills);
           // a rolled loop permuted the accumulators at its back-edge (~170
-          // AGPR moves per iteration): 1.41 -> 1.33 ms
+          // AGPR moves per iteration): 1.41 -> 1.33 ms. The first k-step's W
+          // fragments were loaded before the A -> B barrier (wb0).
+          f16x8 b0[4][3], b1[4][3];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { b0[j][1] = wb0[j][1]; b0[j][2] = wb0[j][2]; }
+          // A fragments one k-step ahead without extra registers: product 1 is
+          // the only reader of the lo plane (A lo x W hi), so the next k-step's
+          // lo fragments are read from LDS into the same registers right after
+          // it, under products 2 and 3; the next hi fragments after product 3,
+          // under the next k-step's product 1. The LDS latency leaves the k-step.
+          auto ld_a = [&](int ks, int pl, f16x8 (&a)[NB][2], f16x8 (&ax)[2]) {
+#pragma unroll
+            for (int mt = 0; mt < NB; ++mt)
+              a[mt][pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * mt * XRH + pl * XKP + 32 * ks);
+            ax[pl] = *reinterpret_cast<const f16x8*>(Ah + 16 * xm * XRH + pl * XKP + 32 * ks);
+          };
+          f16x8 ar[NB][2], arx[2];
+          ld_a(0, 1, ar, arx);
+          ld_a(0, 0, ar, arx);
+          auto kstep_rot = [&](int ks, f16x8 (&bb)[4][3]) {
+            const f16x8 (&a)[NB][2] = ar;
+            const f16x8 (&ax)[2] = arx;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) bb[j][0] = bb[j][2] * (_Float16)kF16LoScale;
+            NRMS_H3STEP2(1, 2)
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + 1 < XKS) ld_a(ks + 1, 1, ar, arx);
+            __builtin_amdgcn_sched_barrier(0);
+            NRMS_H3STEP2(0, 1) NRMS_H3STEP2(0, 0)
+            __builtin_amdgcn_sched_barrier(0);
+            if (ks + 1 < XKS) ld_a(ks + 1, 0, ar, arx);
+          };
+#undef NRMS_H3STEP2
 #pragma unroll
           for (int ks = 0; ks < XKS; ks += 2) {
-            // (each k-step's loads pinned ahead of the other buffer's MFMAs: left
-            // to the scheduler they sank among them and the next k-step waited
-            // for them -- with fewer M-tiles the k-step no longer covered the
-            // L2 latency)
             load_b(ks + 1, b1);
             __builtin_amdgcn_sched_barrier(0);
-            kstep(ks, b0);
+            kstep_rot(ks, b0);
             __builtin_amdgcn_sched_barrier(0);
             if (ks + 2 < XKS) load_b(ks + 2, b0);
             __builtin_amdgcn_sched_barrier(0);
-            kstep(ks + 1, b1);
+            kstep_rot(ks + 1, b1);
             __builtin_amdgcn_sched_barrier(0);
           }
-#endif
           // (the 2^-11 unscale is folded into the epilogue's exp argument)
         } else {
           float4 bb[4], bn4[4];
@@ -1162,7 +1160,8 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         // row), no zero fill. The recheck pass walks groups of any bucket.
 #pragma unroll
         for (int mt = 0; mt < NB; ++mt) {
-          if (!EXACT || mt < nb_next) prefetch_qk_tok(nbuf, mt);
+          if constexpr (!EXACT) prefetch_k_tok(nbuf, mt);
+          else if (mt < nb_next) prefetch_qk_tok(nbuf, mt);
           else zero_qk_tok(mt);
           __builtin_amdgcn_sched_barrier(0);
           float p[4];
@@ -1282,6 +1281,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         // V slices of the next group: issued here, after O is dead (holding both
         // through the B epilogue spills); the S^T phase of the next group covers
         // most of their latency
+        s_carry = stage1(bn3, gn3);   // (issued ahead of the V slices)
         if constexpr (EXACT) {
           prefetch_v(nbuf, nb_next);
         } else {

@@ -55,6 +55,8 @@ def stage_of(name, grid_threads, wg):
         return "pool_news" if blocks > 256 else "pool_user"
     if "score_kernel" in name:
         return "score"
+    if "user_order_kernel" in name:   # the UserEncoder's dispatch order (LPT), part of its stage
+        return "user_order"
     if "fused_user" in name:
         return "user_fused"
     if "fused_news" in name:   # the EXACT recheck launch (true) is its own line
