@@ -579,7 +579,8 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   __syncthreads();
   const int32_t n_groups = __builtin_amdgcn_readfirstlane(sched[2 * NBK + 1]);
   // group k -> bucket (-1 past the end) and the group's index g within it
-  auto bucket_of = [&](int64_t k, int64_t& g) -> int {
+  // (group indices and keys are int32: groups < 2^27, checked at launch)
+  auto bucket_of = [&](int32_t k, int32_t& g) -> int {
     int bsel = -1;
     int32_t start = 0, prev = 0;
 #pragma unroll
@@ -591,49 +592,79 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     g = k - __builtin_amdgcn_readfirstlane(start);
     return __builtin_amdgcn_readfirstlane(bsel);
   };
-  // title of slot t of group g of bucket b (-1: none)
-  auto title_of = [&](int b, int64_t g, int t) -> int32_t {
-    const int64_t c = FT * g + t;
-    if (!ts.list) return c < n_titles ? (int32_t)c : -1;   // (n_titles <= INT32_MAX, checked at launch)
-    const int32_t cbb = sched[NBK + b], rep = sched[2 * NBK];
-    if (c < cbb) return ts.list[b * ts.stride + c];
-    if (b == ts.rep_bucket && c == cbb && rep != INT32_MAX) return rep;
-    return -1;
-  };
   // iteration idx: the group key k and (recheck pass) the mask of titles to write
-  const int64_t n_iter = EXACT ? (int64_t)*rl.count : n_groups;
-  auto key_at = [&](int64_t idx, int& tmask) -> int64_t {
+  const int32_t n_iter = EXACT ? *rl.count : n_groups;
+  auto key_at = [&](int32_t idx, int& tmask) -> int32_t {
     tmask = 0xF;
     if constexpr (EXACT) {
       if (idx >= n_iter) return n_groups;
       const int32_t e = rl.list[idx];
       tmask = e & 0xF;
-      return (int64_t)(e >> 4);
+      return e >> 4;
     }
     return idx;
   };
 
   // Row pointers of a group: slot (t = tid / 20, p = tid % 20) of threads
   // tid < 80, in three stages so that the dependent loads (bucket list ->
-  // compacted row id) hide behind the attention phase: title index, then its
-  // row id and count, then the pointer and the title's (index, count) into LDS.
+  // compacted row id) hide behind other work: the title index, then its row
+  // id and count, then the pointer and the title's (index, count) into LDS.
+  // Each stage issues its loads unconditionally, from a safe address where
+  // there is nothing to load, and the raw values are resolved by the next
+  // stage: a load inside a divergent branch makes the waitcnt pass wait for
+  // every older load (the prefetched gathers) where the branch rejoins.
   const int tslot = tid / FL, pslot = tid - tslot * FL;
-  auto stage1 = [&](int b, int64_t g) -> int32_t { return (tid < FROWS && b >= 0) ? title_of(b, g, tslot) : -1; };
-  auto stage2 = [&](int32_t s, int& c) -> int64_t {
-    c = 0;
-    if (s < 0) return -2;
-    if (ts.crow) {
-      c = ts.cnt[s];
-      return (int64_t)ts.crow[(int64_t)s * FL + pslot];
-    }
-    c = FL;
-    return rmap(s, pslot);
+  struct S1 {
+    int32_t raw;    // list entry (or the title itself without classification)
+    int32_t mode;   // 0: raw, 1: the rep title, 2: no title
   };
-  auto stage3 = [&](int32_t s, int64_t r, int c, int buf) {
+  auto stage1 = [&](int b, int32_t g) -> S1 {
+    const int32_t c = FT * g + tslot;
+    const bool ok = tid < FROWS && b >= 0;
+    S1 x;
+    if (!ts.list) {   // (kernel-uniform)
+      x.raw = c;
+      x.mode = (ok && c < n_titles) ? 0 : 2;   // (n_titles <= INT32_MAX, checked at launch)
+      return x;
+    }
+    const int bb = b >= 0 ? b : 0;
+    const int32_t cbb = sched[NBK + bb], rep = sched[2 * NBK];
+    const bool listed = ok && c < cbb;
+    x.raw = ts.list[listed ? (int64_t)bb * ts.stride + c : 0];
+    x.mode = listed ? 0 : ((ok && b == ts.rep_bucket && c == cbb && rep != INT32_MAX) ? 1 : 2);
+    return x;
+  };
+  auto resolve1 = [&](const S1& x) -> int32_t { return x.mode == 0 ? x.raw : (x.mode == 1 ? sched[2 * NBK] : -1); };
+  struct S2 {
+    int32_t s;       // title (-1: none)
+    int32_t rawc;    // its real-token count (classified)
+    int64_t rawr;    // its compacted row id (classified) or token id / row (RowMap)
+  };
+  auto stage2 = [&](int32_t s) -> S2 {
+    S2 y;
+    y.s = s;
+    const int32_t ss = s < 0 ? 0 : s;   // (title 0 exists: n_titles > 0)
+    if (ts.crow) {   // (kernel-uniform)
+      y.rawc = ts.cnt[ss];
+      y.rawr = ts.crow[(int64_t)ss * FL + pslot];
+    } else {
+      y.rawc = FL;
+      y.rawr = (rmap.direct || !rmap.ids_a) ? (int64_t)ss * FL + pslot : rmap.ids_of(ss)[pslot];
+    }
+    return y;
+  };
+  auto stage3 = [&](const S2& y, int buf) {
+    int c = 0;
+    int64_t r = -2;
+    if (y.s >= 0) {
+      c = y.rawc;
+      r = (ts.crow || rmap.direct || !rmap.ids_a) ? y.rawr
+                                                  : ((uint64_t)y.rawr < (uint64_t)rmap.n_rows ? y.rawr : -1);
+    }
     if (tid < FROWS) {
       rowptr[buf * FROWS + tid] = r == -2 ? zero_row : (r < 0 ? nan_row : qkv + r * ldq);
       if (pslot == 0) {
-        tmeta[8 * buf + tslot] = s;
+        tmeta[8 * buf + tslot] = y.s;
         tmeta[8 * buf + 4 + tslot] = c;
       }
     }
@@ -749,25 +780,22 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 
   // the row pointers of the first two groups (buffers 0 and 1), the title
   // indices of the third (s_carry), then the first group's slices
-  int32_t s_carry = -1;
+  S1 s_carry;
   {
     int b0 = -1;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
       int tm0;
-      int64_t g0 = 0;
-      const int64_t i0 = (int64_t)blockIdx.x + (int64_t)p * gridDim.x;
+      int32_t g0 = 0;
+      const int32_t i0 = (int32_t)blockIdx.x + p * (int32_t)gridDim.x;
       const int b = i0 < n_iter ? bucket_of(key_at(i0, tm0), g0) : -1;
       if (p == 0) b0 = b;
-      int c0;
-      const int32_t s0 = stage1(b, g0);
-      const int64_t r0 = stage2(s0, c0);
-      stage3(s0, r0, c0, p);
+      stage3(stage2(resolve1(stage1(b, g0))), p);
     }
     {
       int tm2;
-      int64_t g2 = 0;
-      const int64_t i2 = (int64_t)blockIdx.x + 2 * (int64_t)gridDim.x;
+      int32_t g2 = 0;
+      const int32_t i2 = (int32_t)blockIdx.x + 2 * (int32_t)gridDim.x;
       s_carry = stage1(i2 < n_iter ? bucket_of(key_at(i2, tm2), g2) : -1, g2);
     }
     __syncthreads();
@@ -791,22 +819,22 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   for (int j = 0; j < 4; ++j) wvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
   f16x8 wb0[4][3];
   // one iteration: group key_at(idx), of bucket NB - 1
-  auto iterate = [&](int64_t idx, auto nbc) {
+  auto iterate = [&](int32_t idx, auto nbc) {
     constexpr int NB = decltype(nbc)::value;
     int tmask, tmask_n;
-    const int64_t k = key_at(idx, tmask);
-    int64_t g, gn = 0;
+    const int32_t k = key_at(idx, tmask);
+    int32_t g, gn = 0;
     bucket_of(k, g);
-    const int64_t kn = key_at(idx + gridDim.x, tmask_n);
-    const int bn = (idx + gridDim.x < n_iter) ? bucket_of(kn, gn) : -1;
+    const int32_t kn = key_at(idx + (int32_t)gridDim.x, tmask_n);
+    const int bn = (idx + (int32_t)gridDim.x < n_iter) ? bucket_of(kn, gn) : -1;
     const int nb_next = bn + 1;   // 0: no next group
     // the group after next has its row pointers staged during this attention
     // (its title indices were read at the end of the previous group: s_carry);
     // the group after that has its title indices read at the end of this one
     int tmask_n3;
-    int64_t gn3 = 0;
-    const int64_t kn3 = key_at(idx + 3 * (int64_t)gridDim.x, tmask_n3);
-    const int bn3 = (idx + 3 * (int64_t)gridDim.x < n_iter) ? bucket_of(kn3, gn3) : -1;
+    int32_t gn3 = 0;
+    const int32_t kn3 = key_at(idx + 3 * (int32_t)gridDim.x, tmask_n3);
+    const int bn3 = (idx + 3 * (int32_t)gridDim.x < n_iter) ? bucket_of(kn3, gn3) : -1;
     // row-pointer buffers: this group's, the next group's, the one after's
     const int buf = it & (RPB - 1), nbuf = (it + 1) & (RPB - 1), nbuf2 = (it + 2) & (RPB - 1);
     {
@@ -830,15 +858,11 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 
       // ---------------- A: attention (4x4x1 MFMA, 16 (title, head) blocks) --------------
       {
-        // the next group's slot rows (stage 1 now, stage 2 after the first
-        // query column, stored at the end of this phase for the prefetch in
-        // this group's B epilogue)
-        // (stage 1, the title index, came from the end of the previous group:
-        // its global load has landed, so stage 2's dependent row-id loads
-        // start at once and are done long before stage 3 at this phase's end)
-        const int32_t s_next = s_carry;
-        int c_next = 0;
-        int64_t r_next = -2;
+        // the slot rows of the group after next: stage 1 (the title index) came
+        // from the end of the previous group, so its load has landed; stage 2's
+        // dependent row-id loads go out after the first query column and are
+        // done long before stage 3 at this phase's end
+        S2 r_next;
         // S^T tiles: rows = keys 4j + r (A = K), cols = queries 4i + x (B = Q)
         floatx4 S[NB][NB];
 #pragma unroll
@@ -950,9 +974,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           s_exp(i);
           o_mfma(i);
           o_store(i);
-          if (i == 0) r_next = stage2(s_next, c_next);
+          if (i == 0) r_next = stage2(resolve1(s_carry));
         }
-        stage3(s_next, r_next, c_next, nbuf2);
+        stage3(r_next, nbuf2);
         if constexpr (H3) {
 #pragma unroll
           for (int pl = 2; pl >= 1; --pl)
@@ -1295,9 +1319,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   };
   if constexpr (EXACT) {
     // flagged groups in list order, any bucket
-    for (int64_t idx = blockIdx.x; idx < n_iter; idx += gridDim.x) {
+    for (int32_t idx = blockIdx.x; idx < n_iter; idx += gridDim.x) {
       int tm;
-      int64_t g;
+      int32_t g;
       switch (bucket_of(key_at(idx, tm), g)) {
         case 0: iterate(idx, std::integral_constant<int, 1>{}); break;
         case 1: iterate(idx, std::integral_constant<int, 2>{}); break;
@@ -1312,10 +1336,10 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     // spilled ~600 registers)
     auto run_bucket = [&](auto nbc) {
       constexpr int NB = decltype(nbc)::value;
-      const int64_t start = NB == NBK ? 0 : __builtin_amdgcn_readfirstlane(sched[NB]);
-      const int64_t end = __builtin_amdgcn_readfirstlane(sched[NB - 1]);
-      const int64_t grid = gridDim.x;
-      int64_t idx = start + (((int64_t)blockIdx.x - start) % grid + grid) % grid;
+      const int32_t start = NB == NBK ? 0 : __builtin_amdgcn_readfirstlane(sched[NB]);
+      const int32_t end = __builtin_amdgcn_readfirstlane(sched[NB - 1]);
+      const int32_t grid = gridDim.x;
+      int32_t idx = start + (((int32_t)blockIdx.x - start) % grid + grid) % grid;
       for (; idx < end; idx += grid) iterate(idx, nbc);
     };
     run_bucket(std::integral_constant<int, 5>{});
