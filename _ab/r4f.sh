@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 set -uo pipefail
 O=gpurun_out/r4f; mkdir -p $O
-bash profiles/probes/ab_news.sh qs1rw qs2 > $O/news_ab.txt 2>&1 || exit 1
+bash profiles/probes/ab_news.sh qs1rw qs2 qs3 > $O/news_ab.txt 2>&1 || exit 1
 timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/ -m gpu > $O/gputests.txt 2>&1 || { tail -30 $O/gputests.txt; exit 1; }
 tail -2 $O/gputests.txt
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.txt 2>&1 || exit 1

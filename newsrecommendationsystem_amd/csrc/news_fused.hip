@@ -638,18 +638,21 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   struct S2 {
     int32_t s;       // title (-1: none)
     int32_t rawc;    // its real-token count (classified)
-    int64_t rawr;    // its compacted row id (classified) or token id / row (RowMap)
+    int32_t rawr;    // its compacted row id (classified; widened in stage 3, after the load)
+    int64_t rawid;   // without classification: its token id (RowMap)
   };
   auto stage2 = [&](int32_t s) -> S2 {
     S2 y;
     y.s = s;
     const int32_t ss = s < 0 ? 0 : s;   // (title 0 exists: n_titles > 0)
+    y.rawc = FL;
+    y.rawr = 0;
+    y.rawid = 0;
     if (ts.crow) {   // (kernel-uniform)
       y.rawc = ts.cnt[ss];
       y.rawr = ts.crow[(int64_t)ss * FL + pslot];
-    } else {
-      y.rawc = FL;
-      y.rawr = (rmap.direct || !rmap.ids_a) ? (int64_t)ss * FL + pslot : rmap.ids_of(ss)[pslot];
+    } else if (!rmap.direct && rmap.ids_a) {
+      y.rawid = rmap.ids_of(ss)[pslot];
     }
     return y;
   };
@@ -658,8 +661,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     int64_t r = -2;
     if (y.s >= 0) {
       c = y.rawc;
-      r = (ts.crow || rmap.direct || !rmap.ids_a) ? y.rawr
-                                                  : ((uint64_t)y.rawr < (uint64_t)rmap.n_rows ? y.rawr : -1);
+      if (ts.crow) r = (int64_t)y.rawr;
+      else if (rmap.direct || !rmap.ids_a) r = (int64_t)y.s * FL + pslot;
+      else r = (uint64_t)y.rawid < (uint64_t)rmap.n_rows ? y.rawid : -1;
     }
     if (tid < FROWS) {
       rowptr[buf * FROWS + tid] = r == -2 ? zero_row : (r < 0 ? nan_row : qkv + r * ldq);
