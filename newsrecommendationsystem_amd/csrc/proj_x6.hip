@@ -268,13 +268,21 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
     const float* p;
     int64_t o;   // output row offset (-1: no row)
   };
-  auto a_src = [&](int64_t rt) __attribute__((always_inline)) -> ASrc {
+  // The row id of the next tile's row is loaded unconditionally (a safe
+  // index past M) and resolved only where the row is loaded, after the
+  // mainloop: consumed at once, its load made the waitcnt pass wait for every
+  // older memory operation -- the previous item's output stores included.
+  auto a_id = [&](int64_t rt) __attribute__((always_inline)) -> int64_t {
+    const int64_t m = rt * PM + ar_;
+    return row_ids ? row_ids[m < M ? m : 0] : m;
+  };
+  auto a_resolve = [&](int64_t rt, int64_t id) __attribute__((always_inline)) -> ASrc {
     const int64_t m = rt * PM + ar_;
     if (m >= M) return ASrc{zero_row, -1};
-    const int64_t id = row_ids ? row_ids[m] : m;
     const int64_t o = (SCATTER ? id : m) * ldy;
     return ASrc{(uint64_t)id < (uint64_t)n_rows_x ? X + ar.offset(id) : nan_row, o};
   };
+  auto a_src = [&](int64_t rt) __attribute__((always_inline)) -> ASrc { return a_resolve(rt, a_id(rt)); };
   float4 ra[AP];
   auto load_a = [&](const float* src) __attribute__((always_inline)) {
 #pragma unroll
@@ -453,8 +461,7 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
       NRMS_PX_STAMP(0)   // (loop overhead, restage of the previous item)
       const int64_t rt = it / PNR;
       const bool restage = it + 1 < i1 && (it + 1) / PNR != rt;   // workgroup-uniform
-      ASrc an{zero_row, -1};
-      if (restage) an = a_src(rt + 1);   // (its id load completes behind the mainloop)
+      const int64_t an_id = restage ? a_id(rt + 1) : 0;   // (its load completes behind the mainloop)
       const int t0 = (int)(it % PNR) * PRANGE + off_w;
       float4 bj[C];
       int4 ej[C];   // H3: column exponents
@@ -574,7 +581,11 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
       for (int j = 0; j < C; ++j) bvoff[j] = bnext[j];
       NRMS_PX_STAMP(2)   // k-steps 1..9
       // the next row tile's A: loads in flight until the restage below
-      if (restage) load_a(an.p);
+      ASrc an{zero_row, -1};
+      if (restage) {
+        an = a_resolve(rt + 1, an_id);
+        load_a(an.p);
+      }
       NRMS_PX_STAMP(3)   // epilogue stores issued
       if (restage) {
         __syncthreads();   // every wave is done with this A tile

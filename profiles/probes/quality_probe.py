@@ -8,7 +8,8 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from newsrecommendationsystem_amd import quality as Q  # noqa: E402
 
-for kw in [dict(steps=320, lr=1e-3, temperature=0.5, dropouts=(0.0, 0.2))]:
+for kw in [dict(steps=320, lr=2e-3, temperature=0.5, dropouts=(0.0, 0.2)),
+           dict(steps=480, lr=1e-3, temperature=0.5, dropouts=(0.0, 0.2))]:
     t0 = time.time()
     r = Q.run_scaled(**kw)
     r["wall_s"] = round(time.time() - t0, 1)
