@@ -234,7 +234,7 @@ def train_clients_reference(init, client_batches, every, device):
 
 
 def run_scaled(steps=320, every=10, world=2, B=128, C=3, V=70976, n_news=20000, dropouts=(0.0, 0.2),
-               lr=1e-3, seed=0, temperature=0.5, eval_impressions=4000):
+               lr=2e-3, seed=0, temperature=0.5, eval_impressions=4000):
     """BASELINE config 5's quality half at the reference's dimensions: V =
     70,976 words, batch 128 (src/config.py:18), 1 + K = 3 candidates, 50
     clicked, `world` FedAvg clients x `steps` local steps, parameters averaged

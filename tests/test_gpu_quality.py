@@ -20,6 +20,6 @@ def test_fedavg_quality_reference_scale():
     assert [r["dropout"] for r in res["runs"]] == [0.0, 0.2]
     for r in res["runs"]:
         assert r["abs_diff_auc"] <= 0.002, r
-        assert r["auc_lift_hip"] >= 0.04, r          # training moved the student (0.050 / 0.044 measured)
-        assert abs(r["auc_reference"] - r["auc_init"]) >= 0.04, r
+        assert r["auc_lift_hip"] >= 0.05, r          # training moved the student (0.056 / 0.052 measured)
+        assert abs(r["auc_reference"] - r["auc_init"]) >= 0.05, r
         assert r["max_normwise_param_diff_excl_WK_bias"] < 5e-3, r
