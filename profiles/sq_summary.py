@@ -37,7 +37,12 @@ def main():
            "valu_per_mfma": round(cs["SQ_INSTS_VALU"] / cs["SQ_INSTS_MFMA"], 3),
            "lds_bank_conflict_cycles": cs.get("SQ_LDS_BANK_CONFLICT"),
            "counters": cs, "source": f"profiles/{tag}_{stage}_sq_counters.txt"}
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sq_counters.json")
+    here = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(here, f"{tag}_{stage}_sq_counters.txt"), "w") as fh:   # (the cited source)
+        fh.write(name + "\n")
+        for c in sorted(acc[name]):
+            fh.write(f"  {c:<32s}{cs[c]:>20.1f}  (n={len(acc[name][c])})\n")
+    path = os.path.join(here, "sq_counters.json")
     try:
         allr = json.load(open(path))
     except (OSError, ValueError):
