@@ -3,6 +3,7 @@
 // caller's stream (no allocation, no synchronisation); the only globals are the
 // process-wide GEMM arithmetic and the once-per-(device, kernel) LDS attribute.
 #include "nrms_common.hpp"
+#include "titles.hpp"
 
 #include <atomic>
 #include <cstdlib>
@@ -122,16 +123,20 @@ size_t news_bytes(const NewsSizes& z) {
 // non-null: row-list mode (launch_gemm_store_list). arith < 0: the current mode.
 int32_t project_qkv(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
                     const nrms_encoder_weights_t* w, float* pack, bool packed, float* Y, int64_t ld,
-                    hipStream_t s, const int32_t* list_count = nullptr, int arith = -1) {
+                    hipStream_t s, const int32_t* list_count = nullptr, int arith = -1,
+                    const tl::TailJobs* tail = nullptr, bool* tail_done = nullptr) {
   const int D = w->d_model;
   const WeightRows wr = qkv_rows(w);
   if (arith < 0) arith = gemm_arith();
   const bool h3 = arith == NRMS_GEMM_SPLIT_F16X3;
+  if (tail_done) *tail_done = false;
   if (pack && arith != NRMS_GEMM_F32 && proj_x6_supported(D, 3 * D, wr) && ((uintptr_t)Y % 16) == 0 &&
       ld % 4 == 0) {
     if (!packed)
       if (int32_t st = launch_proj_x6_pack(wr, pack, nullptr, nullptr, h3, s)) return st;
-    return launch_proj_x6(X, n_rows_x, ar, row_ids, M, pack, Y, ld, list_count, h3, s);
+    const int32_t st = launch_proj_x6(X, n_rows_x, ar, row_ids, M, pack, Y, ld, list_count, h3, s, tail);
+    if (tail_done) *tail_done = st == NRMS_OK && tail != nullptr;
+    return st;
   }
   if (list_count) return launch_gemm_store_list(X, n_rows_x, row_ids, list_count, M, D, wr, 3 * D, Y, ld, s);
   return launch_gemm_store_rows(X, n_rows_x, ar, row_ids, M, D, wr, 3 * D, Y, ld, s);
@@ -144,14 +149,16 @@ int32_t encode_from_qkv(const float* qkv, int64_t ldq, int64_t n_rows, const int
                         const nrms_encoder_weights_t* w, float* ctx, float* scores, float* out,
                         hipStream_t s, float* wap = nullptr, bool* deduped = nullptr,
                         int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0,
-                        bool prepacked = false, bool direct_rows = false, bool* classified = nullptr) {
+                        bool prepacked = false, bool direct_rows = false, bool* classified = nullptr,
+                        bool preclassified = false) {
   const int D = w->d_model;
   if (deduped) *deduped = false;
   if (classified) *classified = false;
   if (wap && fused_news_supported(L, D, w->n_heads, w->query_dim))
     return launch_fused_news(qkv, ldq, n_rows, ids_a, n_seq_a, ids_b, n_seq, w->w_add, w->b_add,
                              w->q_add, wap, out, s, -1, deduped, broadcast_from, user_list, user_rows,
-                             prepacked, direct_rows, -1, classified);
+                             prepacked, direct_rows, -1, classified, preclassified);
+  if (preclassified) return NRMS_ERR_INVALID_ARG;
   if (direct_rows) ids_a = ids_b = nullptr;   // per-token rows: the ids only classify (fused kernel)
   // stage kernels: any row stride >= 3D (packed rows, or the folded table's
   // rows of nrms_qkv_row_stride)
@@ -551,21 +558,30 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   const bool h3 = arith == NRMS_GEMM_SPLIT_F16X3;
   const bool all_packed = packed && folded && user_fused;   // (the fused news tail takes folded + L = 20)
   const bool news_fused_ok = fused_news_supported(L, D, news_w->n_heads, news_w->query_dim);
-  if (all_packed && news_fused_ok) {
-    if ((st = launch_forward_pack(nwr, pack, uwr, upack, news_w->w_add, wap, h3, user_w->w_add, uwap, stream)))
+  const bool prepacked = all_packed && news_fused_ok;
+  // the titles' classification without a launch of its own (titles.hpp): the
+  // first half in the pack launch, the second in the vocabulary projection's tail
+  tl::ClassifyJob cjob{};
+  tl::TailJobs ntail{};
+  const bool split_cls =
+      prepacked && fused_news_classify_split(wap, clicked_ids, n_clk, cand_ids, n_all, V, &cjob, &ntail.sc);
+  if (prepacked) {
+    if ((st = launch_forward_pack(nwr, pack, uwr, upack, news_w->w_add, wap, h3, user_w->w_add, uwap, stream,
+                                  split_cls ? &cjob : nullptr)))
       return st;
   } else if (packed && (st = launch_proj_x6_pack(nwr, pack, &uwr, upack, h3, stream))) {
     return st;
   }
-  const bool prepacked = all_packed && news_fused_ok;
   if (folded) {
+    bool tail_done = false;
     st = project_qkv(table, V, contiguous_rows(D), nullptr, V, news_w, pack, packed, qkv, ld, stream, nullptr,
-                     arith);
+                     arith, split_cls ? &ntail : nullptr, &tail_done);
     if (st) return st;
     if ((st = rec(1))) return st;
+    // (without the tail the news launch classifies the titles itself)
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
                          news, stream, wap, &deduped, bcast_from, user_rows_here ? ulist : nullptr, n_clk,
-                         prepacked, false, &classified);
+                         prepacked, false, &classified, split_cls && tail_done);
   } else {
     st = project_qkv(table, V, contiguous_rows(D), clicked_ids, n_clk * L, news_w, pack, packed, qkv, ld,
                      stream, nullptr, arith);
@@ -590,36 +606,48 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   // other rows are projected (row-list GEMM) and the fused tail reads copied
   // positions from the rep rows. Bitwise the same logits as projecting every row.
   const bool user_dedupe = deduped && user_fused && arith != NRMS_GEMM_F32;
+  // UserEncoder token compaction (user_fused.hip): a user's padding positions
+  // (one news vector) collapse into one row carrying their count
+  const bool user_compact = user_fused && classified && token_compaction() && N <= 64;
   PaddingGroups pg{nullptr, nullptr, nullptr};
   const PaddingGroups pg_all = deduped ? fused_news_padding_groups(wap, n_all) : pg;
+  const PaddingGroups pg_flags = classified ? fused_news_padding_groups(wap, n_all) : pg;
+  // the users' longest-first dispatch order in the projection's tail (titles.hpp)
+  tl::TailJobs utail{};
+  const bool order_tail = user_compact && user_lpt() && B * N <= INT32_MAX;
+  if (order_tail) utail.uo = tl::UserOrder{pg_flags.pad_title, uorder, B, N};
+  bool order_ready = false;
   if (user_dedupe) {
     pg = fused_news_padding_groups(wap, n_all);
     // (listed by the news kernel's prologue in the folded mode; the direct mode
     // has no ids to deduplicate by, so user_dedupe is false there)
     st = project_qkv(news, n_clk, contiguous_rows(D), ulist, n_clk, user_w, upack, packed, uqkv, uld, stream,
-                     pg.user_count, arith);
+                     pg.user_count, arith, order_tail ? &utail : nullptr, &order_ready);
   } else {
     st = project_qkv(news, n_clk, contiguous_rows(D), nullptr, n_clk, user_w, upack, packed, uqkv, uld, stream,
-                     nullptr, arith);
+                     nullptr, arith, order_tail ? &utail : nullptr, &order_ready);
   }
   if (st) return st;
   if ((st = rec(3))) return st;
-  // UserEncoder token compaction (user_fused.hip): a user's padding positions
-  // (one news vector) collapse into one row carrying their count
-  const bool user_compact = user_fused && classified && token_compaction() && N <= 64;
-  const PaddingGroups pg_flags = classified ? fused_news_padding_groups(wap, n_all) : pg;
+  // the click scores in the fused UserEncoder launch (bitwise the score
+  // kernel's; its stage is then empty)
+  const float* cand_news = news + (size_t)n_clk * D;
+  const PaddingGroups* cand_pg = bcast_from == n_all && deduped ? &pg_all : nullptr;
+  const bool score_fold = user_fused && C > 0 && ((uintptr_t)cand_news % 16) == 0;
+  const ScoreFold sfold{cand_news, logits, cand_pg ? *cand_pg : PaddingGroups{nullptr, nullptr, nullptr}, n_clk, C};
   if (user_fused)
     st = launch_fused_user(uqkv, uld, B, N, user_w->w_add, user_w->b_add, user_w->q_add, uwap, user,
                            stream, (user_dedupe || user_compact) ? &pg_flags : nullptr, prepacked, user_dedupe,
-                           user_compact, uorder);
+                           user_compact, uorder, order_ready, score_fold ? &sfold : nullptr);
   else
     st = encode_from_qkv(uqkv, uld, n_clk, nullptr, B, nullptr, B, N, user_w, uctx, uscores, user,
                          stream);
   if (st) return st;
   if ((st = rec(4))) return st;
-  st = launch_score(news + (size_t)n_clk * D, B, C, (int64_t)C * D, D, user, D, D, logits, stream,
-                    bcast_from == n_all && deduped ? &pg_all : nullptr, n_clk);
-  if (st) return st;
+  if (!score_fold) {
+    st = launch_score(cand_news, B, C, (int64_t)C * D, D, user, D, D, logits, stream, cand_pg, n_clk);
+    if (st) return st;
+  }
   return rec(5);
 }
 

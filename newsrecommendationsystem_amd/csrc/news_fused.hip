@@ -38,6 +38,7 @@
 // (M-tile 4, N-tile 12).
 #include "nrms_common.hpp"
 #include "packs.hpp"
+#include "titles.hpp"
 
 #include <atomic>
 #include <cstdlib>
@@ -196,131 +197,19 @@ static_assert(pk::NEWS_COUNTERS == WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS, "pack
 // 4x4x1 MFMA attention's granule) and encoded in groups of 4 titles of one
 // bucket: 16 NB rows, NB M-tiles, NB^2 of the 25 attention tile pairs.
 // Without compaction every title is one 20-row slot (NB = 5).
-constexpr int NBK = 5;                                   // buckets NB = 1..5
+constexpr int NBK = tl::NBK;                             // buckets NB = 1..5
 constexpr int NCNT = pk::NEWS_NCOUNT;                    // int32 counters of a launch
-constexpr int CNT_RECHECK = 0, CNT_BUCKET = 1, CNT_REP = pk::NEWS_CNT_REP, CNT_USER = 7;
-static_assert(CNT_BUCKET + NBK == CNT_REP && CNT_USER < NCNT, "counter layout");
+constexpr int CNT_RECHECK = 0, CNT_BUCKET = tl::CNT_BUCKET, CNT_REP = pk::NEWS_CNT_REP, CNT_USER = 7;
+static_assert(CNT_BUCKET + NBK == CNT_REP && CNT_USER < NCNT && tl::FL == FL, "counter layout");
 
-struct RowMap {
-  const int64_t* ids_a;
-  const int64_t* ids_b;
-  int64_t n_seq_a, n_titles, n_rows;
-  bool direct;   // per-token rows s * FL + i (the per-token projection); ids only classify
-  // q|k|v row of token i of title s: >= 0 row, -1 invalid id (NaN row), -2 no title (zero row)
-  __device__ __forceinline__ int64_t operator()(int64_t s, int i) const {
-    if (s < 0 || s >= n_titles) return -2;
-    if (direct || !ids_a) return s * FL + i;
-    const int64_t id = ids_of(s)[i];
-    return ((uint64_t)id < (uint64_t)n_rows) ? id : -1;
-  }
-  __device__ __forceinline__ const int64_t* ids_of(int64_t s) const {
-    return (s < n_seq_a || ids_b == nullptr) ? ids_a + s * FL : ids_b + (s - n_seq_a) * FL;
-  }
-};
+using tl::RowMap;   // q|k|v row of token i of title s
+using tl::Titles;   // the classification's output
+using tl::CLS_T;
 
-// Classification output (workspace): compacted row ids per title slot, the
-// real-token count, the all-padding flag, per-bucket title lists and counters.
-struct Titles {
-  int32_t* crow;        // [n_titles][FL]: >= 0 row, -1 NaN row (invalid id), -2 zero row (unused slot)
-  uint8_t* cnt;         // [n_titles] c (FL without compaction)
-  uint8_t* pad_title;   // [n_titles] all 20 ids zero
-  int32_t* list;        // [NBK][stride]
-  int32_t* counters;    // [NCNT]
-  int64_t stride;
-};
-
-// One thread per title (10 x 16-B id loads). Lists every title in the bucket
-// of its compacted length, except (dedupe) the all-padding titles: those are
-// one vector, encoded once for the lowest of them (rep, appended to its
-// bucket by the main pass) and copied. One atomicAdd per bucket and one
-// atomicMin per 256-title block (device-scope atomics on one address
-// serialise). List order is arbitrary: a title's result does not depend on the
-// group or slot it is encoded in.
-constexpr int CLS_T = 256, CLS_W = CLS_T / 64;   // (1,024-thread blocks: 55 blocks at config 3, 1.7x slower)
+// Classification as a launch of its own (titles.hpp: classify_block; list
+// entries through one atomicAdd per bucket and one atomicMin per block).
 __global__ __launch_bounds__(CLS_T) void classify_titles_kernel(RowMap rm, Titles tt, int dedupe, int compact) {
-  __shared__ int wcnt[NBK][CLS_W], wbase[NBK][CLS_W], wrep[CLS_W];
-  const int64_t s = (int64_t)blockIdx.x * CLS_T + threadIdx.x;
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  int bucket = -1;
-  bool allpad = false;
-  if (s < rm.n_titles) {
-    const int4* ids4 = reinterpret_cast<const int4*>(rm.ids_of(s));   // 16-B aligned id rows (checked)
-    int64_t id[FL];
-#pragma unroll
-    for (int i = 0; i < FL / 2; ++i) {
-      const int4 v = ids4[i];
-      id[2 * i] = (int64_t)(((uint64_t)(uint32_t)v.y << 32) | (uint32_t)v.x);
-      id[2 * i + 1] = (int64_t)(((uint64_t)(uint32_t)v.w << 32) | (uint32_t)v.z);
-    }
-    auto row = [&](int i) -> int32_t {
-      if (rm.direct) return (int32_t)(s * FL + i);
-      return ((uint64_t)id[i] < (uint64_t)rm.n_rows) ? (int32_t)id[i] : -1;
-    };
-    // the 20 compacted row ids in registers (static indices only: a running
-    // output index spilled the array and turned the stores into 20 scattered
-    // 4-B writes per title), stored as five 16-B writes
-    int32_t out[FL];
-    uint32_t nz = 0;
-#pragma unroll
-    for (int i = 0; i < FL; ++i) nz |= (id[i] != 0 ? 1u : 0u) << i;
-    int c = __popc(nz);
-    if (compact) {
-      // the rep's row: id 0's (folded) or the first padding token's (per token)
-      const int first_pad = __ffs(~nz & ((1u << FL) - 1)) - 1;   // (-1: no padding)
-      const int32_t rep_row = rm.direct ? (int32_t)(s * FL + (first_pad < 0 ? 0 : first_pad))
-                                        : (rm.n_rows > 0 ? 0 : -1);
-#pragma unroll
-      for (int q = 0; q < FL; ++q) out[q] = q == c ? rep_row : -2;
-#pragma unroll
-      for (int i = 0; i < FL; ++i) {
-        const int d = __popc(nz & ((1u << i) - 1));   // real token i's compacted position (<= i)
-        const bool real = (nz >> i) & 1;
-        const int32_t r = row(i);
-#pragma unroll
-        for (int q = 0; q <= i; ++q) out[q] = (real && d == q) ? r : out[q];
-      }
-      const int le = c + (c < FL ? 1 : 0);
-      bucket = (le + 3) / 4 - 1;
-    } else {
-#pragma unroll
-      for (int i = 0; i < FL; ++i) out[i] = row(i);
-      bucket = NBK - 1;
-    }
-    int4* cr4 = reinterpret_cast<int4*>(tt.crow + s * FL);   // (80-B rows, 16-B aligned: workspace)
-#pragma unroll
-    for (int k = 0; k < FL / 4; ++k) cr4[k] = make_int4(out[4 * k], out[4 * k + 1], out[4 * k + 2], out[4 * k + 3]);
-    allpad = c == 0;
-    tt.cnt[s] = (uint8_t)(compact ? c : FL);
-    tt.pad_title[s] = allpad ? 1 : 0;
-    if (dedupe && allpad) bucket = -1;
-  }
-  const uint64_t pads = __ballot(dedupe && allpad);
-  uint64_t bal[NBK];
-#pragma unroll
-  for (int b = 0; b < NBK; ++b) {
-    bal[b] = __ballot(bucket == b);
-    if (lane == 0) wcnt[b][w] = __popcll(bal[b]);
-  }
-  if (lane == 0) wrep[w] = pads ? (int32_t)((int64_t)blockIdx.x * CLS_T + 64 * w + __ffsll((long long)pads) - 1) : INT32_MAX;
-  __syncthreads();
-  if (threadIdx.x < NBK) {
-    const int b = threadIdx.x;
-    int tot = 0;
-    for (int i = 0; i < CLS_W; ++i) tot += wcnt[b][i];
-    int base = tot ? atomicAdd(&tt.counters[CNT_BUCKET + b], tot) : 0;
-    for (int i = 0; i < CLS_W; ++i) { wbase[b][i] = base; base += wcnt[b][i]; }
-  } else if (threadIdx.x == NBK) {
-    int r = INT32_MAX;
-    for (int i = 0; i < CLS_W; ++i) r = min(r, wrep[i]);
-    if (r != INT32_MAX) atomicMin(&tt.counters[CNT_REP], r);
-  }
-  __syncthreads();
-  uint64_t mine = 0;
-  int base = 0;
-#pragma unroll
-  for (int b = 0; b < NBK; ++b)
-    if (bucket == b) { mine = bal[b]; base = wbase[b][w]; }
-  if (bucket >= 0) tt.list[bucket * tt.stride + base + __popcll(mine & ((1ull << lane) - 1))] = (int32_t)s;
+  tl::classify_block<false>(blockIdx.x, threadIdx.x, rm, tt, dedupe, compact, tl::TitleSlots{nullptr, nullptr});
 }
 
 // out[s] = out[rep] for every other all-padding title s >= s0.
@@ -1362,13 +1251,15 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 
 // Workspace after the packed W_add, special rows and f16 planes: int32
 // counters [NCNT] (reset by the pack kernel of every launch), the recheck list
-// (4 per group), the bucket lists [NBK][n], the compacted rows [n][20], then
-// bytes: counts [n] and all-padding flags [n].
+// (4 per group), the bucket lists [NBK][n], the compacted rows [n][20], the
+// split classification's slot codes [n] and block counts [nblk][8] (16-B
+// aligned), then bytes: counts [n] and all-padding flags [n].
 static size_t fused_news_list_offset() { return (size_t)WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS; }
 static int64_t max_groups(int64_t n_titles) { return (n_titles + FT - 1) / FT + NBK; }
 size_t fused_news_workspace_floats(int64_t n_titles) {
   return fused_news_list_offset() + NCNT + 4 * (size_t)max_groups(n_titles) + (size_t)NBK * n_titles + 4 +
-         (size_t)FL * n_titles + ((size_t)2 * n_titles + 3) / 4;
+         (size_t)FL * n_titles + (size_t)n_titles + 4 + (size_t)tl::BLK_INTS * tl::classify_blocks(n_titles) +
+         ((size_t)2 * n_titles + 3) / 4;
 }
 namespace {
 struct NewsWs {
@@ -1376,6 +1267,8 @@ struct NewsWs {
   int32_t* recheck;
   int32_t* list;
   int32_t* crow;
+  int32_t* slot;
+  int32_t* blkcnt;
   uint8_t* cnt;
   uint8_t* pad_title;
 };
@@ -1386,7 +1279,9 @@ NewsWs news_ws(float* ws, int64_t n_titles) {
   z.list = z.recheck + 4 * max_groups(n_titles);
   // (16-B aligned: the classification writes each title's 80-B row as 16-B stores)
   z.crow = reinterpret_cast<int32_t*>((reinterpret_cast<uintptr_t>(z.list + NBK * n_titles) + 15) & ~uintptr_t(15));
-  z.cnt = reinterpret_cast<uint8_t*>(z.crow + FL * n_titles);
+  z.slot = z.crow + FL * n_titles;
+  z.blkcnt = reinterpret_cast<int32_t*>((reinterpret_cast<uintptr_t>(z.slot + n_titles) + 15) & ~uintptr_t(15));
+  z.cnt = reinterpret_cast<uint8_t*>(z.blkcnt + tl::BLK_INTS * tl::classify_blocks(n_titles));
   z.pad_title = z.cnt + n_titles;
   return z;
 }
@@ -1430,12 +1325,46 @@ unsigned long long* g_fused_dbg = nullptr;   // set by profiles/probes/news_vari
 #define NRMS_TIMING_ARG
 #endif
 
+namespace {
+struct ClassifyDecision {
+  bool classify, dedupe, compact;
+};
+// classification (title dedupe and / or token compaction) needs the token ids
+// as 16-B aligned rows, and row ids / title indices that fit int32
+ClassifyDecision classify_decision(const int64_t* ids_a, const int64_t* ids_b, int64_t n_titles, int64_t n_rows,
+                                   bool direct_rows, int dedupe_setting, int compact_setting) {
+  const int dedupe_on = dedupe_setting < 0 ? title_dedupe() : dedupe_setting;
+  const int compact_on = compact_setting < 0 ? token_compaction() : compact_setting;
+  const int64_t row_span = direct_rows ? n_titles * FL : n_rows;
+  const bool classify = ids_a != nullptr && (dedupe_on || compact_on) &&
+                        (((uintptr_t)ids_a | (uintptr_t)(ids_b ? ids_b : ids_a)) % 16) == 0 &&
+                        row_span <= INT32_MAX && n_titles <= INT32_MAX;
+  return {classify, classify && dedupe_on != 0, classify && compact_on != 0};
+}
+}  // namespace
+
+bool fused_news_classify_split(float* ws, const int64_t* ids_a, int64_t n_seq_a, const int64_t* ids_b,
+                               int64_t n_titles, int64_t n_rows, tl::ClassifyJob* job, tl::TitleScatter* sc) {
+  const ClassifyDecision d = classify_decision(ids_a, ids_b, n_titles, n_rows, false, -1, -1);
+  if (!d.classify || n_titles == 0 || ((uintptr_t)ws % 16)) return false;
+  const NewsWs z = news_ws(ws, n_titles);
+  const int64_t nblk = tl::classify_blocks(n_titles);
+  job->rm = RowMap{ids_a, ids_b, n_seq_a, n_titles, n_rows, false};
+  job->tt = Titles{z.crow, z.cnt, z.pad_title, z.list, z.counters, n_titles};
+  job->sl = tl::TitleSlots{z.slot, z.blkcnt};
+  job->dedupe = d.dedupe ? 1 : 0;
+  job->compact = d.compact ? 1 : 0;
+  job->nblk = nblk;
+  *sc = tl::TitleScatter{z.slot, z.blkcnt, z.list, z.counters, n_titles, n_titles, nblk};
+  return true;
+}
+
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
                           int64_t n_seq_a, const int64_t* ids_b, int64_t n_titles,
                           const float* w_add, const float* b_add, const float* q_add, float* ws,
                           float* out, hipStream_t s, int dedupe_setting, bool* deduped,
                           int64_t broadcast_from, int64_t* user_list, int64_t user_rows, bool prepacked,
-                          bool direct_rows, int compact_setting, bool* classified) {
+                          bool direct_rows, int compact_setting, bool* classified, bool preclassified) {
   if (deduped) *deduped = false;
   if (classified) *classified = false;
   if (n_titles == 0) return NRMS_OK;
@@ -1454,16 +1383,10 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   ensure_dynamic_lds(reinterpret_cast<const void*>(kern_exact), (int)lds_bytes_exact);
   const NewsWs z = news_ws(ws, n_titles);
   const RecheckList rl{z.counters + CNT_RECHECK, z.recheck};
-  // classification (title dedupe and / or token compaction) needs the token
-  // ids as 16-B aligned rows, and row ids / title indices that fit int32
-  const int dedupe_on = dedupe_setting < 0 ? title_dedupe() : dedupe_setting;
-  const int compact_on = compact_setting < 0 ? token_compaction() : compact_setting;
-  const int64_t row_span = direct_rows ? n_titles * FL : n_rows;
-  const bool classify = ids_a != nullptr && (dedupe_on || compact_on) &&
-                        (((uintptr_t)ids_a | (uintptr_t)(ids_b ? ids_b : ids_a)) % 16) == 0 &&
-                        row_span <= INT32_MAX && n_titles <= INT32_MAX;
-  const bool dedupe = classify && dedupe_on;
-  const bool compact = classify && compact_on;
+  const ClassifyDecision cd =
+      classify_decision(ids_a, ids_b, n_titles, n_rows, direct_rows, dedupe_setting, compact_setting);
+  const bool classify = cd.classify, dedupe = cd.dedupe, compact = cd.compact;
+  if (preclassified && (!classify || direct_rows || !prepacked)) return NRMS_ERR_INVALID_ARG;
   const TitleSet ts{classify ? z.crow : nullptr, z.cnt, classify ? z.list : nullptr, z.counters, n_titles,
                     compact ? 0 : NBK - 1};
   // the UserEncoder's row list (nrms_forward) in the main pass's prologue
@@ -1494,7 +1417,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   const int64_t groups = classify ? max_groups(n_titles) : (n_titles + FT - 1) / FT;
   const int64_t blocks = groups < n_cu ? groups : n_cu;   // persistent: one workgroup per CU
   const RowMap rm{ids_a, ids_b, n_seq_a, n_titles, n_rows, direct_rows};
-  if (classify) {
+  if (classify && !preclassified) {
     const Titles tt{z.crow, z.cnt, z.pad_title, z.list, z.counters, n_titles};
     hipLaunchKernelGGL(classify_titles_kernel, dim3((unsigned)((n_titles + CLS_T - 1) / CLS_T)), dim3(CLS_T), 0, s,
                        rm, tt, dedupe ? 1 : 0, compact ? 1 : 0);

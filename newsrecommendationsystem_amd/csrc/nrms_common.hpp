@@ -7,6 +7,10 @@
 #include "nrms_hip.h"
 
 namespace nrms {
+namespace tl {
+struct ClassifyJob;
+struct TailJobs;
+}  // namespace tl
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
@@ -185,15 +189,19 @@ size_t proj_x6_pack_floats();
 bool proj_x6_supported(int K, int N, const WeightRows& w);
 int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w1, float* d1, bool h3,
                             hipStream_t s);
+// tail (optional): work every workgroup runs after its items (titles.hpp).
 int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
-                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, bool h3, hipStream_t s);
+                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, bool h3, hipStream_t s,
+                       const tl::TailJobs* tail = nullptr);
 // nrms_forward's weight packings in one launch (split arithmetic): both
 // encoders' Q|K|V (launch_proj_x6_pack layout, h3 = f16), the news W_add into
 // the fused news workspace (f16 planes too when f16) with its counters reset,
-// and the UserEncoder W_add (x6 layout) into its workspace.
+// and the UserEncoder W_add (x6 layout) into its workspace. cls (optional):
+// the first half of the news titles' classification in the same launch
+// (titles.hpp).
 int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& wu, float* pu,
                             const float* news_wadd, float* news_ws, bool f16, const float* user_wadd,
-                            float* user_ws, hipStream_t s);
+                            float* user_ws, hipStream_t s, const tl::ClassifyJob* cls = nullptr);
 int32_t launch_gemm_additive_score(const float* X, int64_t M, int K, const float* W,
                                    const float* b, const float* q, int N, float* score,
                                    hipStream_t s);
@@ -252,10 +260,24 @@ bool fused_user_supported(int L, int D, int H, int Q);
 // (user_fused.hip). order (optional, B int32 of workspace, with compact):
 // the users are dispatched longest compacted length first (NRMS_USER_LPT=0
 // in the environment: in user order).
+// nrms_forward's click scores folded into the UserEncoder launch: logits[b C
+// + c] = news[b C + c] · user[b] in the score kernel's lane order and
+// reduction (score.hip: bitwise its logits), computed by the user's workgroup
+// once its vector is pooled.
+struct ScoreFold {
+  const float* news;   // [B C][D] candidate vectors, 16-B aligned (nullptr: no scores)
+  float* logits;       // [B C]
+  PaddingGroups pg;    // optional: a copied all-padding candidate reads rep's vector
+  int64_t title0;      // title index of candidate 0 (pg)
+  int C;
+};
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
                           hipStream_t s, const PaddingGroups* pg = nullptr, bool prepacked = false,
-                          bool copied = false, bool compact = false, int32_t* order = nullptr);
+                          bool copied = false, bool compact = false, int32_t* order = nullptr,
+                          bool order_ready = false, const ScoreFold* score = nullptr);
+// the longest-first user dispatch order is on (NRMS_USER_LPT, default 1)
+bool user_lpt();
 // Process-wide switch (news_fused.hip): encode one all-padding title per
 // batch and broadcast its vector (nrms_set_title_dedupe; NRMS_DEDUPE=0 in the
 // environment turns it off).
@@ -285,6 +307,9 @@ bool fused_news_supported(int L, int D, int H, int Q);
 // the main pass also builds launch_user_row_list's list of titles
 // 0 .. user_rows - 1 (count in the PaddingGroups user_count). prepacked: ws
 // already holds the packed W_add and reset counters (launch_forward_pack).
+// preclassified: the titles were classified by the forward's split
+// classification (fused_news_classify_split, titles.hpp) -- no classification
+// launch here.
 // direct_rows: the q|k|v rows are per token (row s L + i, the per-token
 // projection); the ids (if any) only classify the tokens.
 int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const int64_t* ids_a,
@@ -293,7 +318,7 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
                           float* out, hipStream_t s, int dedupe_setting = -1, bool* deduped = nullptr,
                           int64_t broadcast_from = 0, int64_t* user_list = nullptr, int64_t user_rows = 0,
                           bool prepacked = false, bool direct_rows = false, int compact_setting = -1,
-                          bool* classified = nullptr);
+                          bool* classified = nullptr, bool preclassified = false);
 PaddingGroups fused_news_padding_groups(float* ws, int64_t n_titles);
 // The rows m < n_rows of titles not copied from rep (the UserEncoder's rows to
 // project), appended to list in any order; their count in *pg.user_count.

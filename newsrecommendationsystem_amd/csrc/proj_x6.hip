@@ -42,6 +42,7 @@
 
 #include "nrms_common.hpp"
 #include "packs.hpp"
+#include "titles.hpp"
 
 #include <type_traits>
 
@@ -178,14 +179,16 @@ __global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, Weight
 // nrms_forward's four packings in one launch: blocks [0, P) news Q|K|V,
 // [P, 2P) user Q|K|V (P = PACK_BLOCKS, or PACK_BLOCKS_H3 when f16), then the
 // news W_add (x6 planes, f16 planes if f16, the special rows, the counters),
-// then the UserEncoder W_add (x6 layout, or split-f16 when f16).
+// then the UserEncoder W_add (x6 layout, or split-f16 when f16), then (cj.nblk
+// > 0) the first half of the news titles' classification (titles.hpp).
 constexpr int PACK_BLOCKS = (PACK_ELEMS + 255) / 256;
 constexpr int NEWS_ADD_BLOCKS = (pk::NEWS_X6_ELEMS + pk::NEWS_SPECIAL + 255) / 256;
 constexpr int USER_ADD_BLOCKS = (pk::USER_X6_ELEMS + 255) / 256;
 __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float* __restrict__ pn, WeightRows wu,
                                                            float* __restrict__ pu, const float* __restrict__ nwa,
                                                            float* __restrict__ nws, int nf16,
-                                                           const float* __restrict__ uwa, float* __restrict__ uws) {
+                                                           const float* __restrict__ uwa, float* __restrict__ uws,
+                                                           tl::ClassifyJob cj) {
   int b = blockIdx.x;
   const int t = threadIdx.x;
   if (nf16) {
@@ -206,8 +209,15 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
     return;
   }
   b -= NEWS_ADD_BLOCKS;
-  if (nf16) pk::pack_user_additive_h3(b, t, uwa, uws);
-  else pk::pack_user_additive(b * 256 + t, uwa, uws, 1);
+  const int ub = nf16 ? pk::USER_H3_BLOCKS : USER_ADD_BLOCKS;
+  if (b < ub) {
+    if (nf16) pk::pack_user_additive_h3(b, t, uwa, uws);
+    else pk::pack_user_additive(b * 256 + t, uwa, uws, 1);
+    return;
+  }
+  b -= ub;
+  static_assert(tl::CLS_T == 256, "classification blocks of the pack launch");
+  tl::classify_block<true>(b, t, cj.rm, cj.tt, cj.dedupe, cj.compact, cj.sl);
 }
 
 // SCATTER: output row m goes to Y row row_ids[m] (row-list mode; the count is
@@ -222,7 +232,8 @@ template <bool SCATTER, int NW, bool H3>
 __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __restrict__ X, int64_t n_rows_x, ARows ar,
                                                             const int64_t* __restrict__ row_ids, int64_t M,
                                                             const float* __restrict__ packed, float* __restrict__ Y,
-                                                            int64_t ldy, const int32_t* __restrict__ m_dev) {
+                                                            int64_t ldy, const int32_t* __restrict__ m_dev,
+                                                            tl::TailJobs tj) {
   static_assert(NW == 4 || NW == 8, "waves per workgroup");
   constexpr int NTH = 64 * NW;
   constexpr int TPR = NTH / PM;                      // threads per A row (4 or 8)
@@ -241,7 +252,11 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
   const int64_t n_items = (M + PM - 1) / PM * PNR;
   const int64_t i0 = (int64_t)blockIdx.x * n_items / gridDim.x;
   const int64_t i1 = ((int64_t)blockIdx.x + 1) * n_items / gridDim.x;
-  if (i0 >= i1) return;
+  const bool tail = tj.sc.slot || tj.uo.pad;
+  if (i0 >= i1) {
+    if (tail) tl::run_tail_jobs<NTH>(tj, threadIdx.x);
+    return;
+  }
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int lm = lane & 15, kq = lane >> 4;
@@ -600,6 +615,7 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
   if constexpr (NW == 4) run(std::integral_constant<int, PTW>{});
   else if (w < 4) run(std::integral_constant<int, 3>{});
   else run(std::integral_constant<int, 2>{});
+  if (tail) tl::run_tail_jobs<NTH>(tj, tid);
 #ifdef NRMS_PX_TIMING
   if (lane == 0) {
     unsigned long long* dbg = reinterpret_cast<unsigned long long*>(const_cast<float*>(packed) + OFF_STAMP);
@@ -626,32 +642,37 @@ int32_t launch_proj_x6_pack(const WeightRows& w0, float* d0, const WeightRows* w
 
 int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& wu, float* pu,
                             const float* news_wadd, float* news_ws, bool f16, const float* user_wadd,
-                            float* user_ws, hipStream_t s) {
+                            float* user_ws, hipStream_t s, const tl::ClassifyJob* cls) {
   if (((uintptr_t)pn | (uintptr_t)pu) % 16) return NRMS_ERR_UNSUPPORTED;
-  const int blocks = 2 * (f16 ? PACK_BLOCKS_H3 : PACK_BLOCKS) + NEWS_ADD_BLOCKS +
-                     (f16 ? pk::USER_H3_BLOCKS : USER_ADD_BLOCKS);
-  hipLaunchKernelGGL(forward_pack_kernel, dim3(blocks), dim3(256), 0, s, wn, pn, wu, pu, news_wadd, news_ws,
-                     f16 ? 1 : 0, user_wadd, user_ws);
+  tl::ClassifyJob cj{};
+  if (cls) cj = *cls;
+  const int64_t blocks = 2 * (f16 ? PACK_BLOCKS_H3 : PACK_BLOCKS) + NEWS_ADD_BLOCKS +
+                         (f16 ? pk::USER_H3_BLOCKS : USER_ADD_BLOCKS) + (cls ? cj.nblk : 0);
+  if (blocks > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(forward_pack_kernel, dim3((unsigned)blocks), dim3(256), 0, s, wn, pn, wu, pu, news_wadd,
+                     news_ws, f16 ? 1 : 0, user_wadd, user_ws, cj);
   return launch_status();
 }
 
 namespace {
 template <bool SCATTER, bool H3>
 void launch_proj_kernel(int64_t grid, const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
-                        const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, hipStream_t s) {
+                        const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, const tl::TailJobs& tj,
+                        hipStream_t s) {
 #ifndef NRMS_PX_WAVES
 #define NRMS_PX_WAVES 8
 #endif
   constexpr int NW = NRMS_PX_WAVES;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_qkv_kernel<SCATTER, NW, H3>), (int)P_LDS);
   hipLaunchKernelGGL((proj_qkv_kernel<SCATTER, NW, H3>), dim3((unsigned)grid), dim3(64 * NW), P_LDS, s, X, n_rows_x,
-                     ar, row_ids, M, packed, Y, ldy, m_dev);
+                     ar, row_ids, M, packed, Y, ldy, m_dev, tj);
 }
 }  // namespace
 
 int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
-                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, bool h3, hipStream_t s) {
-  if (M == 0) return NRMS_OK;
+                       const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, bool h3, hipStream_t s,
+                       const tl::TailJobs* tail) {
+  if (M == 0 && !tail) return NRMS_OK;
   if (((uintptr_t)X % 16) || ((uintptr_t)packed % 16) || ar.stride_row % 4 ||
       (ar.per_batch != INT64_MAX && ar.stride_batch % 4) || ldy < PN || ((uintptr_t)Y % 16) || ldy % 4)
     return NRMS_ERR_UNSUPPORTED;
@@ -662,13 +683,16 @@ int32_t launch_proj_x6(const float* X, int64_t n_rows_x, ARows ar, const int64_t
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) n_cu = v;
   }
   const int64_t items = (M + PM - 1) / PM * PNR;
-  const int64_t grid = items < n_cu ? items : n_cu;   // persistent: one workgroup per CU
+  // persistent: one workgroup per CU (every CU with tail jobs: they are spread
+  // over the grid)
+  const int64_t grid = tail ? n_cu : (items < n_cu ? items : n_cu);
+  const tl::TailJobs tj = tail ? *tail : tl::TailJobs{};
   if (m_dev) {
-    if (h3) launch_proj_kernel<true, true>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, m_dev, s);
-    else launch_proj_kernel<true, false>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, m_dev, s);
+    if (h3) launch_proj_kernel<true, true>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, m_dev, tj, s);
+    else launch_proj_kernel<true, false>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, m_dev, tj, s);
   } else {
-    if (h3) launch_proj_kernel<false, true>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, nullptr, s);
-    else launch_proj_kernel<false, false>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, nullptr, s);
+    if (h3) launch_proj_kernel<false, true>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, nullptr, tj, s);
+    else launch_proj_kernel<false, false>(grid, X, n_rows_x, ar, row_ids, M, packed, Y, ldy, nullptr, tj, s);
   }
   return launch_status();
 }

@@ -136,7 +136,7 @@ template <int MODE, int LMAX, int NT>
 __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     const float* __restrict__ qkv, int64_t ldq, int L_all, const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
-    PaddingGroups pg, int uflags, const int32_t* __restrict__ order) {
+    PaddingGroups pg, int uflags, const int32_t* __restrict__ order, ScoreFold sf) {
   static_assert(NT >= UH * LMAX, "one (head, query) task per thread");
   constexpr int NW = NT / 64;
   constexpr int NTPW = (UNT + NW - 1) / NW;            // N-tiles per wave
@@ -552,6 +552,25 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   }
   __syncthreads();
   NRMS_U_STAMP(4)   // softmax
+  // click scores (ScoreFold): wave c < C loads candidate c's vector now, under
+  // the pooling (lane i holds float4 columns i and i + 64, the score kernel's)
+  const bool scoring = sf.news != nullptr;
+  auto cand_vec = [&](int c) -> const float4* {
+    const int64_t pair = s * sf.C + c;
+    const float* nv = sf.news + pair * UD;
+    if (sf.pg.pad_title) {
+      const int64_t t = sf.title0 + pair, r = *sf.pg.rep;
+      if (sf.pg.pad_title[t] && t != r) nv = sf.news + (r - sf.title0) * UD;
+    }
+    return reinterpret_cast<const float4*>(nv);
+  };
+  float4 cn[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+  if (scoring && w < sf.C) {
+    const float4* n4 = cand_vec(w);
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
+      if (lane + 64 * k < UD / 4) cn[k] = n4[lane + 64 * k];
+  }
   // PP lanes per float4 column (rows i = par mod PP each), combined by lane
   // shuffles: 8 per column (600 lanes) when the workgroup has them
   constexpr int PP = NT >= 8 * (UD / 4) ? 8 : (NT >= 4 * (UD / 4) ? 4 : 2);
@@ -599,7 +618,35 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       o.z += __shfl_xor(o.z, m);
       o.w += __shfl_xor(o.w, m);
     }
-    if (u < UD / 4 && par == 0) reinterpret_cast<float4*>(out + s * UD)[u] = o;
+    if (u < UD / 4 && par == 0) {
+      reinterpret_cast<float4*>(out + s * UD)[u] = o;
+      if (scoring) reinterpret_cast<float4*>(part)[u] = o;   // (part is free after the softmax)
+    }
+  }
+  if (scoring) {
+    __syncthreads();
+    const float4* u4 = reinterpret_cast<const float4*>(part);
+    for (int c = w; c < sf.C; c += NW) {   // (uniform per wave)
+      if (c != w) {
+        const float4* n4 = cand_vec(c);
+#pragma unroll
+        for (int k = 0; k < 2; ++k)
+          if (lane + 64 * k < UD / 4) cn[k] = n4[lane + 64 * k];
+      }
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (lane + 64 * k < UD / 4) {
+          const float4 a = cn[k], uu = u4[lane + 64 * k];
+          acc = fmaf(a.x, uu.x, acc);
+          acc = fmaf(a.y, uu.y, acc);
+          acc = fmaf(a.z, uu.z, acc);
+          acc = fmaf(a.w, uu.w, acc);
+        }
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) sf.logits[s * sf.C + c] = acc;
+    }
   }
 #ifdef NRMS_USER_TIMING
   NRMS_U_STAMP(5)   // pooling
@@ -613,22 +660,22 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 template <int MODE, int LMAX, int NT>
 int32_t launch_user_inst(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
-                         PaddingGroups pg, int uflags, const int32_t* order) {
+                         PaddingGroups pg, int uflags, const int32_t* order, const ScoreFold& sf) {
   const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64 + 2 * 64) * 4;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>), (int)lds);
   hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
-                     ldq, L, wap, b_add, q_add, out, pg, uflags, order);
+                     ldq, L, wap, b_add, q_add, out, pg, uflags, order, sf);
   return launch_status();
 }
 
 template <int MODE>
 int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
-                         PaddingGroups pg, int uflags, const int32_t* order) {
-  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order);
-  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order);
-  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order);
-  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order);
+                         PaddingGroups pg, int uflags, const int32_t* order, const ScoreFold& sf) {
+  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
+  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
+  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
+  return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
 }
 
 }  // namespace
@@ -640,6 +687,7 @@ static std::atomic<int> g_user_lpt{[] {
   return (e && e[0] == '0') ? 0 : 1;
 }()};
 int set_user_lpt(int on) { return g_user_lpt.exchange(on ? 1 : 0); }
+bool user_lpt() { return g_user_lpt.load(std::memory_order_relaxed) != 0; }
 
 bool fused_user_supported(int L, int D, int H, int Q) {
   return L >= 1 && L <= 64 && D == UD && H == UH && Q == UQ;
@@ -648,7 +696,7 @@ bool fused_user_supported(int L, int D, int H, int Q) {
 int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const float* w_add,
                           const float* b_add, const float* q_add, float* wap, float* out,
                           hipStream_t s, const PaddingGroups* pgp, bool prepacked, bool copied, bool compact,
-                          int32_t* order) {
+                          int32_t* order, bool order_ready, const ScoreFold* score) {
   const PaddingGroups pg = pgp ? *pgp : PaddingGroups{nullptr, nullptr, nullptr};
   if (compact && (!pgp || L > 64 || B * L > INT32_MAX)) return NRMS_ERR_UNSUPPORTED;
   if (copied && !pgp) return NRMS_ERR_INVALID_ARG;
@@ -657,6 +705,12 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16 || ldq < 3 * UD || ldq % 4)
     return NRMS_ERR_UNSUPPORTED;
+  ScoreFold sf{};
+  if (score && score->C > 0) {
+    if (!score->news || !score->logits || ((uintptr_t)score->news % 16)) return NRMS_ERR_INVALID_ARG;
+    if (score->pg.pad_title && !score->pg.rep) return NRMS_ERR_INVALID_ARG;
+    sf = *score;
+  }
   const int ar = gemm_arith();
   const int mode = ar == NRMS_GEMM_F32 ? 0 : (ar == NRMS_GEMM_SPLIT_F16X3 ? 2 : 1);
   if (!prepacked) {
@@ -666,15 +720,17 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
   }
   // longest users first (compaction only: Le comes from the padding flags)
   const int32_t* ord = nullptr;
-  if (compact && order && g_user_lpt.load(std::memory_order_relaxed)) {
+  if (compact && order && order_ready) {
+    ord = order;   // (computed by the UserEncoder projection's tail, titles.hpp)
+  } else if (compact && order && g_user_lpt.load(std::memory_order_relaxed)) {
     hipLaunchKernelGGL(user_order_kernel, dim3((unsigned)((B + UORD_T - 1) / UORD_T)), dim3(UORD_T), 0, s,
                        pg.pad_title, B, L, order);
     if (int32_t st = launch_status()) return st;
     ord = order;
   }
-  if (mode == 2) return launch_user_mode<2>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord);
-  if (mode == 1) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord);
-  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord);
+  if (mode == 2) return launch_user_mode<2>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord, sf);
+  if (mode == 1) return launch_user_mode<1>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord, sf);
+  return launch_user_mode<0>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, ord, sf);
 }
 
 }  // namespace nrms
