@@ -23,6 +23,17 @@ static int initial_gemm_arith() {
   return NRMS_GEMM_SPLIT_F16X3;
 }
 static std::atomic<int> g_gemm_arith{initial_gemm_arith()};
+// A/B switches of nrms_forward's launch folding (default on; "0" turns off):
+// NRMS_SPLIT_CLASSIFY -- the titles' classification in the pack launch and the
+// vocabulary projection's tail (titles.hpp) instead of a launch of its own
+// (the user dispatch order moves with it); NRMS_SCORE_FOLD -- the click scores
+// in the UserEncoder launch instead of the score kernel.
+static bool env_on(const char* name) {
+  const char* e = getenv(name);
+  return !(e && e[0] == '0');
+}
+static const bool g_split_classify = env_on("NRMS_SPLIT_CLASSIFY");
+static const bool g_score_fold = env_on("NRMS_SCORE_FOLD");
 static thread_local int32_t t_gemm_arith = -1;   // nrms_set_thread_gemm_arith (-1: none)
 int gemm_arith() {
   const int32_t t = t_gemm_arith;
@@ -564,7 +575,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   tl::ClassifyJob cjob{};
   tl::TailJobs ntail{};
   const bool split_cls =
-      prepacked && fused_news_classify_split(wap, clicked_ids, n_clk, cand_ids, n_all, V, &cjob, &ntail.sc);
+      g_split_classify && prepacked && fused_news_classify_split(wap, clicked_ids, n_clk, cand_ids, n_all, V, &cjob, &ntail.sc);
   if (prepacked) {
     if ((st = launch_forward_pack(nwr, pack, uwr, upack, news_w->w_add, wap, h3, user_w->w_add, uwap, stream,
                                   split_cls ? &cjob : nullptr)))
@@ -614,7 +625,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   const PaddingGroups pg_flags = classified ? fused_news_padding_groups(wap, n_all) : pg;
   // the users' longest-first dispatch order in the projection's tail (titles.hpp)
   tl::TailJobs utail{};
-  const bool order_tail = user_compact && user_lpt() && B * N <= INT32_MAX;
+  const bool order_tail = g_split_classify && user_compact && user_lpt() && B * N <= INT32_MAX;
   if (order_tail) utail.uo = tl::UserOrder{pg_flags.pad_title, uorder, B, N};
   bool order_ready = false;
   if (user_dedupe) {
@@ -633,7 +644,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   // kernel's; its stage is then empty)
   const float* cand_news = news + (size_t)n_clk * D;
   const PaddingGroups* cand_pg = bcast_from == n_all && deduped ? &pg_all : nullptr;
-  const bool score_fold = user_fused && C > 0 && ((uintptr_t)cand_news % 16) == 0;
+  const bool score_fold = g_score_fold && user_fused && C > 0 && ((uintptr_t)cand_news % 16) == 0;
   const ScoreFold sfold{cand_news, logits, cand_pg ? *cand_pg : PaddingGroups{nullptr, nullptr, nullptr}, n_clk, C};
   if (user_fused)
     st = launch_fused_user(uqkv, uld, B, N, user_w->w_add, user_w->b_add, user_w->q_add, uwap, user,

@@ -179,8 +179,9 @@ __global__ __launch_bounds__(256) void proj_x6_pack_kernel(WeightRows w0, Weight
 // nrms_forward's four packings in one launch: blocks [0, P) news Q|K|V,
 // [P, 2P) user Q|K|V (P = PACK_BLOCKS, or PACK_BLOCKS_H3 when f16), then the
 // news W_add (x6 planes, f16 planes if f16, the special rows, the counters),
-// then the UserEncoder W_add (x6 layout, or split-f16 when f16), then (cj.nblk
-// > 0) the first half of the news titles' classification (titles.hpp).
+// then the UserEncoder W_add (x6 layout, or split-f16 when f16); before all of
+// them (cj.nblk > 0) the first half of the news titles' classification
+// (titles.hpp).
 constexpr int PACK_BLOCKS = (PACK_ELEMS + 255) / 256;
 constexpr int NEWS_ADD_BLOCKS = (pk::NEWS_X6_ELEMS + pk::NEWS_SPECIAL + 255) / 256;
 constexpr int USER_ADD_BLOCKS = (pk::USER_X6_ELEMS + 255) / 256;
@@ -191,6 +192,10 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
                                                            tl::ClassifyJob cj) {
   int b = blockIdx.x;
   const int t = threadIdx.x;
+  // the classification blocks first (their id loads are the launch's long
+  // pole; dispatched last they set its end)
+  if (b < cj.nblk) return tl::classify_block<true>(b, t, cj.rm, cj.tt, cj.dedupe, cj.compact, cj.sl);
+  b -= (int)cj.nblk;
   if (nf16) {
     if (b < PACK_BLOCKS_H3) return pack_proj_h3(b, t, wn, pn);
     b -= PACK_BLOCKS_H3;
@@ -209,15 +214,9 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
     return;
   }
   b -= NEWS_ADD_BLOCKS;
-  const int ub = nf16 ? pk::USER_H3_BLOCKS : USER_ADD_BLOCKS;
-  if (b < ub) {
-    if (nf16) pk::pack_user_additive_h3(b, t, uwa, uws);
-    else pk::pack_user_additive(b * 256 + t, uwa, uws, 1);
-    return;
-  }
-  b -= ub;
+  if (nf16) pk::pack_user_additive_h3(b, t, uwa, uws);
+  else pk::pack_user_additive(b * 256 + t, uwa, uws, 1);
   static_assert(tl::CLS_T == 256, "classification blocks of the pack launch");
-  tl::classify_block<true>(b, t, cj.rm, cj.tt, cj.dedupe, cj.compact, cj.sl);
 }
 
 // SCATTER: output row m goes to Y row row_ids[m] (row-list mode; the count is
@@ -363,6 +362,9 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
   {
     const ASrc a0 = a_src(i0 / PNR);
     load_a(a0.p);
+    // the tail jobs (titles.hpp) under the first A tile's loads: after the
+    // last item they added their dependent loads to the kernel's end
+    if (tail) tl::run_tail_jobs<NTH>(tj, tid);
     store_a(a0.o);
   }
   __syncthreads();
@@ -615,7 +617,6 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
   if constexpr (NW == 4) run(std::integral_constant<int, PTW>{});
   else if (w < 4) run(std::integral_constant<int, 3>{});
   else run(std::integral_constant<int, 2>{});
-  if (tail) tl::run_tail_jobs<NTH>(tj, tid);
 #ifdef NRMS_PX_TIMING
   if (lane == 0) {
     unsigned long long* dbg = reinterpret_cast<unsigned long long*>(const_cast<float*>(packed) + OFF_STAMP);

@@ -14,8 +14,8 @@
 //     compacted rows, counts and flags as before, and instead of list entries
 //     a slot code per title (bucket << 16 | rank among the block's titles of
 //     that bucket) and the block's bucket counts and lowest all-padding title;
-//   B (the tail of the vocabulary projection, proj_qkv_kernel: every
-//     workgroup, after its last item) -- each workgroup takes a contiguous
+//   B (the "tail jobs" of the vocabulary projection, proj_qkv_kernel: every
+//     workgroup, under the loads of its first A tile) -- each workgroup takes a contiguous
 //     range of classification blocks, sums the counts of the blocks before
 //     its range, and writes its titles into the bucket lists; workgroup 0
 //     writes the bucket totals and the rep title into the counters; the
@@ -228,8 +228,7 @@ __device__ __forceinline__ int wg_min(int v, int* red, int tid) {
   return t;
 }
 
-// Every thread of the workgroup calls this (after the workgroup's own work;
-// it synchronises the workgroup).
+// Every thread of the workgroup calls this (it synchronises the workgroup).
 template <int NTH>
 __device__ __forceinline__ void run_tail_jobs(const TailJobs& tj, int tid) {
   __shared__ int red[NTH / 64];
