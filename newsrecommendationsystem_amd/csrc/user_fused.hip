@@ -207,6 +207,24 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       const float4 v = qp[t];
       q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
     }
+#ifdef NRMS_UKV_GLDS
+    // LDS-DMA (global_load_lds_dwordx4): the tile's rows are the K|V rows
+    // back to back (2,400 B each), so wave-instruction p fills bytes
+    // 1,024 p .. + 1,023 of it, each lane from its own row; lanes past the
+    // last row reload its last 16 B into the LDS after the tile (part, free
+    // until the attention's end)
+    {
+      const int nbytes = L * URS * 4;
+      const int npieces = (nbytes + 1023) >> 10;
+      for (int p = w; p < npieces; p += NT / 64) {
+        int o = (p << 10) + 16 * lane;
+        o = o < nbytes ? o : nbytes - 16;
+        const int i = o / (URS * 4), wb = o - i * (URS * 4);
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(row(i) + UD + (wb >> 2)),
+                                         (__attribute__((address_space(3))) void*)(tile + (p << 8)), 16, 0, 0);
+      }
+    }
+#else
     constexpr int KV4 = URS / 4;                               // float4 per K|V row
     constexpr int PER = (LMAX * KV4 + NT - 1) / NT;
     float4 buf[PER];
@@ -223,6 +241,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       const int i = e / KV4, c = e - i * KV4;
       if (e < L * KV4) *reinterpret_cast<float4*>(tile + i * URS + 4 * c) = buf[k];
     }
+#endif
   }
   static_assert(MODE != 2 || UNT * 64 + 64 + 64 >= UH * LMAX, "per-thread max slots before rexp");
   __syncthreads();
@@ -422,6 +441,52 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     if constexpr (MODE == 2) {
       const uf16x8* Bq = reinterpret_cast<const uf16x8*>(WaP) + lane;
       const _Float16* t16 = reinterpret_cast<const _Float16*>(tile);
+#ifdef NRMS_UGEMM_PIPE
+      // W fragments one k-step ahead (an L2 round trip per k-step was the
+      // phase's latency: 6.7 k cycles even for one M-tile)
+      uf16x8 bc[NTPW][2], bn[NTPW][2];
+      auto load_bk = [&](int ks, uf16x8 (&dst)[NTPW][2]) __attribute__((always_inline)) {
+#pragma unroll
+        for (int j = 0; j < NTPW; ++j) {
+          const int nt = w + NW * j < UNT ? w + NW * j : UNT - 1;   // (tiles past N: not used)
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl) dst[j][pl] = Bq[((ks * UNT + nt) * 2 + pl) * 64];
+        }
+      };
+      load_bk(0, bc);
+#pragma unroll
+      for (int ks = 0; ks < UKS; ++ks) {
+        if (ks + 1 < UKS) load_bk(ks + 1, bn);
+        uf16x8 a[MT][2];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int pl = 0; pl < 2; ++pl)
+            a[mt][pl] = *reinterpret_cast<const uf16x8*>(t16 + 2 * arow[mt] + UKP * pl + 32 * ks + 8 * kq);
+#pragma unroll
+        for (int j = 0; j < NTPW; ++j) {
+          const int nt = w + NW * j;
+          if (nt >= UNT) break;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0], bc[j][1], c[mt][j], 0, 0, 0);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][1], bc[j][0], c[mt][j], 0, 0, 0);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0] * (_Float16)kF16LoScale, bc[j][0], c[mt][j],
+                                                                0, 0, 0);
+        }
+        if (ks + 1 < UKS) {
+#pragma unroll
+          for (int j = 0; j < NTPW; ++j) {
+            bc[j][0] = bn[j][0];
+            bc[j][1] = bn[j][1];
+          }
+        }
+      }
+#else
       for (int ks = 0; ks < UKS; ++ks) {
         uf16x8 a[MT][2];
 #pragma unroll
@@ -448,6 +513,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
                                                                 0, 0);
         }
       }
+#endif
     } else if constexpr (MODE == 1) {
       const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
       const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile);
