@@ -207,12 +207,12 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       const float4 v = qp[t];
       q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
     }
-#ifdef NRMS_UKV_GLDS
     // LDS-DMA (global_load_lds_dwordx4): the tile's rows are the K|V rows
     // back to back (2,400 B each), so wave-instruction p fills bytes
     // 1,024 p .. + 1,023 of it, each lane from its own row; lanes past the
-    // last row reload its last 16 B into the LDS after the tile (part, free
-    // until the attention's end)
+    // last row reload its last 16 B into the LDS after the L rows (unused
+    // rows, or part: free until the attention's end). (Register staging:
+    // user_fused 2.1 us slower, profiles/r4m_user_staging_gemm_ab.txt)
     {
       const int nbytes = L * URS * 4;
       const int npieces = (nbytes + 1023) >> 10;
@@ -224,24 +224,6 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
                                          (__attribute__((address_space(3))) void*)(tile + (p << 8)), 16, 0, 0);
       }
     }
-#else
-    constexpr int KV4 = URS / 4;                               // float4 per K|V row
-    constexpr int PER = (LMAX * KV4 + NT - 1) / NT;
-    float4 buf[PER];
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + k * NT;
-      const int i = e / KV4, c = e - i * KV4;
-      buf[k] = e < L * KV4 ? *reinterpret_cast<const float4*>(row(i) + UD + 4 * c)
-                           : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int k = 0; k < PER; ++k) {
-      const int e = tid + k * NT;
-      const int i = e / KV4, c = e - i * KV4;
-      if (e < L * KV4) *reinterpret_cast<float4*>(tile + i * URS + 4 * c) = buf[k];
-    }
-#endif
   }
   static_assert(MODE != 2 || UNT * 64 + 64 + 64 >= UH * LMAX, "per-thread max slots before rexp");
   __syncthreads();
@@ -344,6 +326,19 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   }
   __syncthreads();   // every K|V read done: the tile becomes the context
   NRMS_U_STAMP(1)   // attention
+#ifdef NRMS_UB0_EARLY
+  // the GEMM's first W fragments, in flight under the context split
+  uf16x8 bfirst[NTPW][2];
+  if constexpr (MODE == 2) {
+    const uf16x8* Bq0 = reinterpret_cast<const uf16x8*>(WaP) + lane;
+#pragma unroll
+    for (int j = 0; j < NTPW; ++j) {
+      const int nt = w + NW * j < UNT ? w + NW * j : UNT - 1;
+#pragma unroll
+      for (int pl = 0; pl < 2; ++pl) bfirst[j][pl] = Bq0[(nt * 2 + pl) * 64];
+    }
+  }
+#endif
   if constexpr (MODE == 2) {
     // three fp16 planes per row (hi | lo | r), in the MODE 1 positions
     _Float16* t16 = reinterpret_cast<_Float16*>(tile);
@@ -441,7 +436,6 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     if constexpr (MODE == 2) {
       const uf16x8* Bq = reinterpret_cast<const uf16x8*>(WaP) + lane;
       const _Float16* t16 = reinterpret_cast<const _Float16*>(tile);
-#ifdef NRMS_UGEMM_PIPE
       // W fragments one k-step ahead (an L2 round trip per k-step was the
       // phase's latency: 6.7 k cycles even for one M-tile)
       uf16x8 bc[NTPW][2], bn[NTPW][2];
@@ -453,7 +447,15 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
           for (int pl = 0; pl < 2; ++pl) dst[j][pl] = Bq[((ks * UNT + nt) * 2 + pl) * 64];
         }
       };
+#ifdef NRMS_UB0_EARLY
+#pragma unroll
+      for (int j = 0; j < NTPW; ++j) {
+        bc[j][0] = bfirst[j][0];
+        bc[j][1] = bfirst[j][1];
+      }
+#else
       load_bk(0, bc);
+#endif
 #pragma unroll
       for (int ks = 0; ks < UKS; ++ks) {
         if (ks + 1 < UKS) load_bk(ks + 1, bn);
@@ -486,34 +488,6 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
           }
         }
       }
-#else
-      for (int ks = 0; ks < UKS; ++ks) {
-        uf16x8 a[MT][2];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int pl = 0; pl < 2; ++pl)
-            a[mt][pl] = *reinterpret_cast<const uf16x8*>(t16 + 2 * arow[mt] + UKP * pl + 32 * ks + 8 * kq);
-#pragma unroll
-        for (int j = 0; j < NTPW; ++j) {
-          const int nt = w + NW * j;
-          if (nt >= UNT) break;
-          uf16x8 b[2];
-#pragma unroll
-          for (int pl = 0; pl < 2; ++pl) b[pl] = Bq[((ks * UNT + nt) * 2 + pl) * 64];
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0], b[1], c[mt][j], 0, 0, 0);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][1], b[0], c[mt][j], 0, 0, 0);
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-            c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0] * (_Float16)kF16LoScale, b[0], c[mt][j], 0,
-                                                                0, 0);
-        }
-      }
-#endif
     } else if constexpr (MODE == 1) {
       const bf16x8* Bq = reinterpret_cast<const bf16x8*>(WaP) + lane;
       const uint16_t* t16 = reinterpret_cast<const uint16_t*>(tile);
