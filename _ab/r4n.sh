@@ -1,0 +1,8 @@
+#!/usr/bin/env bash
+set -uo pipefail
+O=gpurun_out/r4n; mkdir -p $O
+NRMS_LIB_PATH=_ab/lib_ub0.so timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "user or forward or plan" > $O/tests_ub0.txt 2>&1 || { tail -30 $O/tests_ub0.txt; exit 1; }
+tail -n 1 $O/tests_ub0.txt
+bash _ab/ab_stage.sh _ab/lib_cur.so _ab/lib_ub0.so > $O/ab.txt 2>&1 || exit 1
+bash _ab/ab_stage.sh _ab/lib_cur.so _ab/lib_ub0.so >> $O/ab.txt 2>&1 || exit 1
+cat $O/ab.txt

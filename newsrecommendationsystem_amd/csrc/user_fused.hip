@@ -235,28 +235,31 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     // exp(d / sqrt(d_k)) as v_exp_f32(d · log2(e) / sqrt(d_k)), as the news kernel
     const float rs = 1.4426950408889634f / sqrtf((float)UDK);
     const float sqrt_dk = sqrtf((float)UDK);
+    // packed FP32 (v_pk_fma_f32, two FMAs per lane per instruction): the dot
+    // product as even / odd partial sums added at the end, the context update
+    // elementwise (the same FMAs as the scalar form): user_fused -1.3 us
+    // (profiles/r4o_user_pk_fma_ab.txt)
+    typedef float f2 __attribute__((ext_vector_type(2)));
     auto dot = [&](int j) __attribute__((always_inline)) {
       const float4* kr = reinterpret_cast<const float4*>(tile + j * URS + UDK * h);
-      float d = 0.f;
+      f2 d = f2{0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
         const float4 k4 = kr[t];
-        d = fmaf(q[4 * t], k4.x, d);
-        d = fmaf(q[4 * t + 1], k4.y, d);
-        d = fmaf(q[4 * t + 2], k4.z, d);
-        d = fmaf(q[4 * t + 3], k4.w, d);
+        d = __builtin_elementwise_fma(f2{q[4 * t], q[4 * t + 1]}, f2{k4.x, k4.y}, d);
+        d = __builtin_elementwise_fma(f2{q[4 * t + 2], q[4 * t + 3]}, f2{k4.z, k4.w}, d);
       }
-      return d;
+      return d.x + d.y;
     };
     auto axpy = [&](float a, int j) __attribute__((always_inline)) {
       const float4* vr = reinterpret_cast<const float4*>(tile + j * URS + UD + UDK * h);
+      const f2 a2 = f2{a, a};
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
         const float4 v4 = vr[t];
-        acc[4 * t] = fmaf(a, v4.x, acc[4 * t]);
-        acc[4 * t + 1] = fmaf(a, v4.y, acc[4 * t + 1]);
-        acc[4 * t + 2] = fmaf(a, v4.z, acc[4 * t + 2]);
-        acc[4 * t + 3] = fmaf(a, v4.w, acc[4 * t + 3]);
+        const f2 lo = __builtin_elementwise_fma(a2, f2{v4.x, v4.y}, f2{acc[4 * t], acc[4 * t + 1]});
+        const f2 hi = __builtin_elementwise_fma(a2, f2{v4.z, v4.w}, f2{acc[4 * t + 2], acc[4 * t + 3]});
+        acc[4 * t] = lo.x; acc[4 * t + 1] = lo.y; acc[4 * t + 2] = hi.x; acc[4 * t + 3] = hi.y;
       }
     };
 #pragma unroll
@@ -326,19 +329,6 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   }
   __syncthreads();   // every K|V read done: the tile becomes the context
   NRMS_U_STAMP(1)   // attention
-#ifdef NRMS_UB0_EARLY
-  // the GEMM's first W fragments, in flight under the context split
-  uf16x8 bfirst[NTPW][2];
-  if constexpr (MODE == 2) {
-    const uf16x8* Bq0 = reinterpret_cast<const uf16x8*>(WaP) + lane;
-#pragma unroll
-    for (int j = 0; j < NTPW; ++j) {
-      const int nt = w + NW * j < UNT ? w + NW * j : UNT - 1;
-#pragma unroll
-      for (int pl = 0; pl < 2; ++pl) bfirst[j][pl] = Bq0[(nt * 2 + pl) * 64];
-    }
-  }
-#endif
   if constexpr (MODE == 2) {
     // three fp16 planes per row (hi | lo | r), in the MODE 1 positions
     _Float16* t16 = reinterpret_cast<_Float16*>(tile);
@@ -447,15 +437,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
           for (int pl = 0; pl < 2; ++pl) dst[j][pl] = Bq[((ks * UNT + nt) * 2 + pl) * 64];
         }
       };
-#ifdef NRMS_UB0_EARLY
-#pragma unroll
-      for (int j = 0; j < NTPW; ++j) {
-        bc[j][0] = bfirst[j][0];
-        bc[j][1] = bfirst[j][1];
-      }
-#else
       load_bk(0, bc);
-#endif
 #pragma unroll
       for (int ks = 0; ks < UKS; ++ks) {
         if (ks + 1 < UKS) load_bk(ks + 1, bn);
