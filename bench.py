@@ -645,7 +645,10 @@ def main():
         "user_rows_encoded": user_rows[0],
         "stages_note": f"HIP events recorded by the library between its stages, a separate pass of "
                        f"{n_ev} steps after the timed ones (events cost queue time, so the timed steps "
-                       f"run without them)",
+                       f"run without them). nrms_forward folds the click scores into the UserEncoder "
+                       f"launch and the title classification into the pack launch and the vocabulary "
+                       f"projection (qkv_news): 'score' is then an empty event pair, 'user_fused' "
+                       f"includes the scoring",
         "user_rows_projected": n_user,
         "timed_path": ("nrms_forward (one C-ABI call) captured once in a HIP graph, replayed per step"
                        if graph is not None else
