@@ -532,12 +532,8 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
 #ifdef NRMS_PX_NOSTORE   // probe: the epilogue without its stores
           if (v.x == 12345.f) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
 #else
-#ifdef NRMS_PX_NTSTORE
-          if (full || 16 * (t0 + j) + 4 * kq < PN)
-            __builtin_nontemporal_store(floatx4{v.x, v.y, v.z, v.w}, reinterpret_cast<floatx4*>(base[mt] + 16 * j));
-#else
+          // (non-temporal stores: qkv_news 0.26 vs 0.16 ms, profiles/r4q_proj_store_waves_ab.txt)
           if (full || 16 * (t0 + j) + 4 * kq < PN) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
-#endif
 #endif
         }
       };
