@@ -575,9 +575,7 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
   tl::ClassifyJob cjob{};
   tl::TailJobs ntail{};
   const bool split_cls =
-      g_split_classify && prepacked &&
-      fused_news_classify_split(wap, clicked_ids, n_clk, cand_ids, n_all, V, &cjob, &ntail.sc,
-                                user_rows_here ? ulist : nullptr, n_clk);
+      g_split_classify && prepacked && fused_news_classify_split(wap, clicked_ids, n_clk, cand_ids, n_all, V, &cjob, &ntail.sc);
   if (prepacked) {
     if ((st = launch_forward_pack(nwr, pack, uwr, upack, news_w->w_add, wap, h3, user_w->w_add, uwap, stream,
                                   split_cls ? &cjob : nullptr)))
@@ -592,12 +590,9 @@ int32_t forward_impl(const int64_t* cand_ids, const int64_t* clicked_ids, int64_
     if (st) return st;
     if ((st = rec(1))) return st;
     // (without the tail the news launch classifies the titles itself)
-    // (the tail also wrote the UserEncoder's row list: ntail.sc.user_list)
-    const bool pre = split_cls && tail_done;
     st = encode_from_qkv(qkv, ld, V, clicked_ids, n_clk, cand_ids, n_all, L, news_w, ctx, scores,
-                         news, stream, wap, &deduped, bcast_from,
-                         user_rows_here && !(pre && ntail.sc.user_list) ? ulist : nullptr, n_clk, prepacked,
-                         false, &classified, pre);
+                         news, stream, wap, &deduped, bcast_from, user_rows_here ? ulist : nullptr, n_clk,
+                         prepacked, false, &classified, split_cls && tail_done);
   } else {
     st = project_qkv(table, V, contiguous_rows(D), clicked_ids, n_clk * L, news_w, pack, packed, qkv, ld,
                      stream, nullptr, arith);

@@ -199,7 +199,7 @@ static_assert(pk::NEWS_COUNTERS == WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS, "pack
 // Without compaction every title is one 20-row slot (NB = 5).
 constexpr int NBK = tl::NBK;                             // buckets NB = 1..5
 constexpr int NCNT = pk::NEWS_NCOUNT;                    // int32 counters of a launch
-constexpr int CNT_RECHECK = 0, CNT_BUCKET = tl::CNT_BUCKET, CNT_REP = pk::NEWS_CNT_REP, CNT_USER = tl::CNT_USER;
+constexpr int CNT_RECHECK = 0, CNT_BUCKET = tl::CNT_BUCKET, CNT_REP = pk::NEWS_CNT_REP, CNT_USER = 7;
 static_assert(CNT_BUCKET + NBK == CNT_REP && CNT_USER < NCNT && tl::FL == FL, "counter layout");
 
 using tl::RowMap;   // q|k|v row of token i of title s
@@ -1344,24 +1344,18 @@ ClassifyDecision classify_decision(const int64_t* ids_a, const int64_t* ids_b, i
 }  // namespace
 
 bool fused_news_classify_split(float* ws, const int64_t* ids_a, int64_t n_seq_a, const int64_t* ids_b,
-                               int64_t n_titles, int64_t n_rows, tl::ClassifyJob* job, tl::TitleScatter* sc,
-                               int64_t* user_list, int64_t n_user) {
+                               int64_t n_titles, int64_t n_rows, tl::ClassifyJob* job, tl::TitleScatter* sc) {
   const ClassifyDecision d = classify_decision(ids_a, ids_b, n_titles, n_rows, false, -1, -1);
   if (!d.classify || n_titles == 0 || ((uintptr_t)ws % 16)) return false;
   const NewsWs z = news_ws(ws, n_titles);
   const int64_t nblk = tl::classify_blocks(n_titles);
   job->rm = RowMap{ids_a, ids_b, n_seq_a, n_titles, n_rows, false};
   job->tt = Titles{z.crow, z.cnt, z.pad_title, z.list, z.counters, n_titles};
-  // (the UserEncoder's row list: only after a deduplicating launch, as the
-  // news kernel's prologue builds it)
-  const bool ul = d.dedupe && user_list != nullptr && n_user > 0;
-  const int64_t nu = ul ? (n_user < n_titles ? n_user : n_titles) : 0;
-  job->sl = tl::TitleSlots{z.slot, z.blkcnt, nu};
+  job->sl = tl::TitleSlots{z.slot, z.blkcnt};
   job->dedupe = d.dedupe ? 1 : 0;
   job->compact = d.compact ? 1 : 0;
   job->nblk = nblk;
-  *sc = tl::TitleScatter{z.slot, z.blkcnt, z.list, z.counters, n_titles, n_titles, nblk, z.pad_title,
-                         ul ? user_list : nullptr, nu};
+  *sc = tl::TitleScatter{z.slot, z.blkcnt, z.list, z.counters, n_titles, n_titles, nblk};
   return true;
 }
 

@@ -12,18 +12,13 @@
 //   A (forward_pack_kernel, proj_x6.hip: extra blocks next to the weight
 //     packing) -- each block of CLS_T titles classifies its titles, writes the
 //     compacted rows, counts and flags as before, and instead of list entries
-//     a slot code per title (its bucket and rank among the block's titles of
-//     that bucket; its rank among the block's UserEncoder rows) and the
-//     block's bucket counts, lowest all-padding title and UserEncoder-row
-//     count;
+//     a slot code per title (bucket << 16 | rank among the block's titles of
+//     that bucket) and the block's bucket counts and lowest all-padding title;
 //   B (the "tail jobs" of the vocabulary projection, proj_qkv_kernel: every
 //     workgroup, under the loads of its first A tile) -- each workgroup takes a contiguous
 //     range of classification blocks, sums the counts of the blocks before
 //     its range, and writes its titles into the bucket lists; workgroup 0
-//     writes the bucket totals, the rep title and the UserEncoder's row count
-//     into the counters; with dedupe the workgroups also write the
-//     UserEncoder's row list (the clicked titles not copied from rep, in title
-//     order; the news kernel's prologue built it with atomics before); the
+//     writes the bucket totals and the rep title into the counters; the
 //     UserEncoder's dispatch order is computed in the tail of the UserEncoder's
 //     projection.
 // The list order is then fixed (block order, ranks within blocks): a title's
@@ -41,13 +36,7 @@ constexpr int FL = 20;                          // tokens per title (config.num_
 constexpr int NBK = 5;                          // buckets NB = ceil(Le / 4) = 1 .. 5
 constexpr int CLS_T = 256, CLS_W = CLS_T / 64;  // titles per classification block
 constexpr int CNT_BUCKET = 1, CNT_REP = pk::NEWS_CNT_REP;
-constexpr int BLK_INTS = 8;   // per block: 5 bucket counts, lowest all-padding title, UserEncoder rows, 1 unused
-constexpr int BLK_UROWS = 6;
-// slot code: bits 0-7 rank in the bucket, 8-15 rank among the block's
-// UserEncoder rows (titles < n_user, not all-padding), 16-18 bucket, bit 20
-// listed in a bucket
-constexpr int SLOT_LISTED = 1 << 20;
-constexpr int CNT_USER = 7;
+constexpr int BLK_INTS = 8;                     // per block: 5 bucket counts, lowest all-padding title, 2 unused
 
 struct RowMap {
   const int64_t* ids_a;
@@ -77,11 +66,10 @@ struct Titles {
   int64_t stride;
 };
 
-// Split mode (half A): slot code per title and per-block counts.
+// Split mode (half A): slot code per title (-1: not listed) and per-block counts.
 struct TitleSlots {
   int32_t* slot;     // [n_titles]
   int32_t* blkcnt;   // [nblk][BLK_INTS] (16-B aligned)
-  int64_t n_user;    // titles 0 .. n_user - 1 are the UserEncoder's rows (0: none)
 };
 
 __host__ __device__ constexpr int64_t classify_blocks(int64_t n_titles) { return (n_titles + CLS_T - 1) / CLS_T; }
@@ -151,9 +139,6 @@ __device__ __forceinline__ void classify_block(int64_t blk, int tid, const RowMa
     tt.pad_title[s] = allpad ? 1 : 0;
     if (dedupe && allpad) bucket = -1;
   }
-  // (split) the block's UserEncoder rows before this title: titles < n_user
-  // that are not all-padding (the rep among them is added by half B)
-  const uint64_t urow = __ballot(SPLIT && s < sl.n_user && s < rm.n_titles && !allpad);
   const uint64_t pads = __ballot(dedupe && allpad);
   uint64_t bal[NBK];
 #pragma unroll
@@ -162,8 +147,6 @@ __device__ __forceinline__ void classify_block(int64_t blk, int tid, const RowMa
     if (lane == 0) wcnt[b][w] = __popcll(bal[b]);
   }
   if (lane == 0) wrep[w] = pads ? (int32_t)(blk * CLS_T + 64 * w + __ffsll((long long)pads) - 1) : INT32_MAX;
-  __shared__ int wurow[CLS_W];
-  if (SPLIT && lane == 0) wurow[w] = __popcll(urow);
   __syncthreads();
   if (tid < NBK) {
     const int b = tid;
@@ -178,10 +161,6 @@ __device__ __forceinline__ void classify_block(int64_t blk, int tid, const RowMa
     for (int i = 0; i < CLS_W; ++i) r = min(r, wrep[i]);
     if constexpr (SPLIT) sl.blkcnt[blk * BLK_INTS + NBK] = r;
     else if (r != INT32_MAX) atomicMin(&tt.counters[CNT_REP], r);
-  } else if (SPLIT && tid == NBK + 1) {
-    int u = 0;
-    for (int i = 0; i < CLS_W; ++i) u += wurow[i];
-    sl.blkcnt[blk * BLK_INTS + BLK_UROWS] = u;
   }
   __syncthreads();
   uint64_t mine = 0;
@@ -191,10 +170,7 @@ __device__ __forceinline__ void classify_block(int64_t blk, int tid, const RowMa
     if (bucket == b) { mine = bal[b]; base = wbase[b][w]; }
   const int rank = base + __popcll(mine & ((1ull << lane) - 1));
   if constexpr (SPLIT) {
-    int ubase = 0;
-    for (int i = 0; i < CLS_W; ++i) ubase += i < w ? wurow[i] : 0;
-    const int urank = ubase + __popcll(urow & ((1ull << lane) - 1));
-    if (s < rm.n_titles) sl.slot[s] = (bucket >= 0 ? (SLOT_LISTED | bucket << 16 | rank) : 0) | urank << 8;
+    if (s < rm.n_titles) sl.slot[s] = bucket >= 0 ? (bucket << 16 | rank) : -1;
   } else {
     if (bucket >= 0) tt.list[bucket * tt.stride + rank] = (int32_t)s;
   }
@@ -207,9 +183,6 @@ struct TitleScatter {
   int32_t* list;
   int32_t* counters;
   int64_t stride, n_titles, nblk;
-  const uint8_t* pad_title;
-  int64_t* user_list;      // nullptr: no UserEncoder row list; else its rows: titles < n_user
-  int64_t n_user;
 };
 
 // The UserEncoder's dispatch order (user_fused.hip): longest compacted length
@@ -265,13 +238,13 @@ __device__ __forceinline__ void run_tail_jobs(const TailJobs& tj, int tid) {
     const int64_t c0 = g * sc.nblk / G, c1 = (g + 1) * sc.nblk / G;
     const bool totals = g == 0;
     if (c0 < c1 || totals) {
-      // bucket and UserEncoder-row offsets of block c0 (sums over the blocks
-      // before it), the rep (every workgroup: its UserEncoder row), and the
-      // totals (workgroup 0: over every block)
-      int pre[NBK], tot[NBK], rep = INT32_MAX, upre = 0, utot = 0;
+      // bucket offsets of block c0 (sum over the blocks before it), and the
+      // totals and the rep (workgroup 0: over every block)
+      int pre[NBK], tot[NBK], rep = INT32_MAX;
 #pragma unroll
       for (int b = 0; b < NBK; ++b) pre[b] = tot[b] = 0;
-      for (int64_t j = tid; j < sc.nblk; j += NTH) {
+      const int64_t jend = totals ? sc.nblk : c0;
+      for (int64_t j = tid; j < jend; j += NTH) {
         const int4 x = *reinterpret_cast<const int4*>(sc.blkcnt + j * BLK_INTS);
         const int4 y = *reinterpret_cast<const int4*>(sc.blkcnt + j * BLK_INTS + 4);
         const int v[NBK] = {x.x, x.y, x.z, x.w, y.x};
@@ -280,19 +253,14 @@ __device__ __forceinline__ void run_tail_jobs(const TailJobs& tj, int tid) {
           pre[b] += j < c0 ? v[b] : 0;
           tot[b] += v[b];
         }
-        upre += j < c0 ? y.z : 0;
-        utot += y.z;
         rep = min(rep, y.y);
       }
 #pragma unroll
       for (int b = 0; b < NBK; ++b) pre[b] = wg_sum<NTH>(pre[b], red, tid);
-      rep = wg_min<NTH>(rep, red, tid);
-      const bool ulist = sc.user_list != nullptr;
-      if (ulist) upre = wg_sum<NTH>(upre, red, tid);
       if (totals) {
 #pragma unroll
         for (int b = 0; b < NBK; ++b) tot[b] = wg_sum<NTH>(tot[b], red, tid);
-        utot = wg_sum<NTH>(utot, red, tid);
+        rep = wg_min<NTH>(rep, red, tid);
         if (tid < NBK) {
           int t = 0;
 #pragma unroll
@@ -300,30 +268,23 @@ __device__ __forceinline__ void run_tail_jobs(const TailJobs& tj, int tid) {
           sc.counters[CNT_BUCKET + tid] = t;
         } else if (tid == NBK) {
           sc.counters[CNT_REP] = rep;
-        } else if (tid == NBK + 1 && ulist) {
-          sc.counters[CNT_USER] = utot + ((int64_t)rep < sc.n_user ? 1 : 0);
         }
       }
       for (int64_t blk = c0; blk < c1; ++blk) {
-        // the rep's UserEncoder row sits at its title position
-        const int ushift = (int64_t)rep < blk * CLS_T ? 1 : 0;
         for (int t = tid; t < CLS_T; t += NTH) {
           const int64_t s = blk * CLS_T + t;
-          const int32_t code = s < sc.n_titles ? sc.slot[s] : 0;
-          if (code & SLOT_LISTED) {
-            const int b = (code >> 16) & 7;
+          const int32_t code = s < sc.n_titles ? sc.slot[s] : -1;
+          if (code >= 0) {
+            const int b = code >> 16;
             int base = 0;
 #pragma unroll
             for (int q = 0; q < NBK; ++q) base = b == q ? pre[q] : base;
-            sc.list[b * sc.stride + base + (code & 0xff)] = (int32_t)s;
+            sc.list[b * sc.stride + base + (code & 0xffff)] = (int32_t)s;
           }
-          if (ulist && s < sc.n_user && (!sc.pad_title[s] || s == rep))
-            sc.user_list[upre + ushift + ((code >> 8) & 0xff) + (rep < s && (int64_t)rep >= blk * CLS_T ? 1 : 0)] = s;
         }
         const int4 x = *reinterpret_cast<const int4*>(sc.blkcnt + blk * BLK_INTS);
-        const int4 y = *reinterpret_cast<const int4*>(sc.blkcnt + blk * BLK_INTS + 4);
-        pre[0] += x.x; pre[1] += x.y; pre[2] += x.z; pre[3] += x.w; pre[4] += y.x;
-        upre += y.z;
+        const int y = sc.blkcnt[blk * BLK_INTS + 4];
+        pre[0] += x.x; pre[1] += x.y; pre[2] += x.z; pre[3] += x.w; pre[4] += y;
       }
     }
   }
@@ -380,11 +341,7 @@ struct ClassifyJob {
 // launch on workspace ws (news_fused.hip): false when launch_fused_news would
 // not classify them; else both halves' arguments. The news launch then takes
 // preclassified = true (and prepacked: the pack's counter reset comes first).
-// user_list (optional, n_user rows): the UserEncoder's row list is written
-// by the tail as well (with dedupe; its count into the counters) -- the news
-// launch then takes user_list = nullptr.
 bool fused_news_classify_split(float* ws, const int64_t* ids_a, int64_t n_seq_a, const int64_t* ids_b,
-                               int64_t n_titles, int64_t n_rows, tl::ClassifyJob* job, tl::TitleScatter* sc,
-                               int64_t* user_list = nullptr, int64_t n_user = 0);
+                               int64_t n_titles, int64_t n_rows, tl::ClassifyJob* job, tl::TitleScatter* sc);
 
 }  // namespace nrms
