@@ -41,8 +41,10 @@ def _newer(src_paths, dst):
 
 
 def _deps():
-    return [os.path.join(CSRC, "nrms_common.hpp"), os.path.join(INCLUDE, "nrms_hip.h"),
-            os.path.abspath(__file__)]   # flag changes rebuild too
+    # every header of csrc/ (a source whose header changed must recompile: a
+    # stale object compiled against an older struct layout links silently)
+    hdrs = sorted(os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h")))
+    return hdrs + [os.path.join(INCLUDE, "nrms_hip.h"), os.path.abspath(__file__)]   # flag changes rebuild too
 
 
 def build(force=False, verbose=True):
