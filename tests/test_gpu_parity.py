@@ -526,6 +526,30 @@ def test_plan_matches_forward(device, fused, mode, gemm_mode):
     assert np.abs(_np(y) - O.forward(cand, clk, sd, np.float64)).max() <= TOL * np.abs(_np(y)).max()
 
 
+def test_plan_matches_forward_many_classification_blocks(device):
+    """nrms_forward's split classification (titles.hpp) with more 256-title
+    classification blocks than projection workgroups (B = 1,536: 84,480
+    titles, 330 blocks over 256 CUs) and a quarter of the history titles all
+    padding (rep, copies, UserEncoder row list): logits bitwise those of the
+    stage calls, which classify in a launch of their own with atomics
+    (pipeline.ForwardPlan)."""
+    from newsrecommendationsystem_amd.pipeline import ForwardPlan
+    V, B = 3000, 1536
+    sd = W.nrms_state(9, V)
+    m = _module(sd, V, device)
+    cand, clk, _ = W.impressions(9, 78, B, V)
+    clk = clk.copy()
+    rng = np.random.default_rng(9)
+    clk[rng.random(clk.shape[:2]) < 0.25] = 0
+    c, k = torch.from_numpy(cand).to(device), torch.from_numpy(clk).to(device)
+    plan = ForwardPlan(m, B, 5, 50, 20, proj_mode=2, fused=True)
+    with torch.no_grad():
+        y = plan.run(c, k).clone()
+        ref = m.forward_ids(c, k, proj_mode=2)
+    assert torch.isfinite(ref).all()
+    assert torch.equal(y, ref)
+
+
 def test_split_gemm_accuracy_matches_f32(device):
     """The split GEMMs are as accurate as the exact-f32 MFMA GEMMs: against
     the fp64 oracle, the x6 and f16x3 forwards' errors are within 2x the f32
