@@ -383,6 +383,10 @@ def main():
     ap.add_argument("--unfused", action="store_true", help="separate MHSA / additive / pool kernels")
     ap.add_argument("--no-extras", action="store_true", help="skip the gather / config-2 / direct figures")
     ap.add_argument("--no-graph", action="store_true", help="time the eager call loop instead of a HIP graph replay")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="batches in flight: that many captured forwards (own workspace, logits and stream) "
+                         "replayed in turn, so one batch's launch boundaries and kernel tails overlap "
+                         "another's kernels (graph path only)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend for the barrier / max-over-ranks timing (nccl = RCCL); "
                          "gloo lets several ranks share one GPU for a rehearsal")
@@ -469,19 +473,28 @@ def main():
         # HIP graph (the C ABI is capturable: no allocation, no sync) and
         # replayed, as a serving loop would; the eager loop is timed beside it.
         graph = None
+        graphs, gstreams = [], []
         if not args.unfused and not args.stream and len(full) == 1 and not args.no_graph:
-            side = torch.cuda.Stream(device)
-            side.wait_stream(torch.cuda.current_stream(device))
-            with torch.cuda.stream(side):
-                fwd.run(cand, clk)
-            torch.cuda.current_stream(device).wait_stream(side)
-            graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graph):
-                fwd.run(cand, clk)
-            fwd.logits.fill_(float("nan"))     # the replay must recompute them
-            graph.replay()
-            torch.cuda.synchronize()
-            same = same and bool(torch.equal(fwd.logits, y_fwd))
+            # (--inflight K: K forwards, each with its own workspace, logits,
+            # graph and stream; replayed in turn)
+            fwds = [fwd] + [TimedForward(model, B, C, N_CLICKED, L, proj_mode=mode)
+                            for _ in range(max(1, args.inflight) - 1)]
+            for f in fwds:
+                side = torch.cuda.Stream(device)
+                side.wait_stream(torch.cuda.current_stream(device))
+                with torch.cuda.stream(side):
+                    f.run(cand, clk)
+                torch.cuda.current_stream(device).wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    f.run(cand, clk)
+                f.logits.fill_(float("nan"))     # the replay must recompute them
+                g.replay()
+                torch.cuda.synchronize()
+                same = same and bool(torch.equal(f.logits, y_fwd))
+                graphs.append(g)
+                gstreams.append(torch.cuda.Stream(device))
+            graph = graphs[0]
         eager_ms = None
         if graph is not None:
             torch.cuda.synchronize()
@@ -494,7 +507,14 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if graph is not None:
+        if graph is not None and len(graphs) > 1:
+            cur = torch.cuda.current_stream(device)
+            for st in gstreams:
+                st.wait_stream(cur)
+            for k in range(steps):
+                with torch.cuda.stream(gstreams[k % len(graphs)]):
+                    graphs[k % len(graphs)].replay()
+        elif graph is not None:
             for _ in range(steps):
                 graph.replay()
         else:
@@ -626,7 +646,8 @@ def main():
                    "news_tail": "unfused" if args.unfused else "fused",
                    "stream": {"impressions": args.stream_impressions or S.N_IMPRESSIONS,
                               "users": S.N_USERS, "sharding": "user_id % world"},
-                   "parallelism": f"user-shard x{world}"},
+                   "parallelism": f"user-shard x{world}",
+                   "batches_in_flight": max(1, len(graphs))},
         "roofline": roofline,
         "titles": {"per_step": n_titles, "all_padding": n_pad, "encoded": n_enc,
                    "rows_encoded": news_rows[0], "rows_if_uncompacted": n_enc * L,
@@ -650,7 +671,10 @@ def main():
                        f"projection (qkv_news): 'score' is then an empty event pair, 'user_fused' "
                        f"includes the scoring",
         "user_rows_projected": n_user,
-        "timed_path": ("nrms_forward (one C-ABI call) captured once in a HIP graph, replayed per step"
+        "timed_path": (("nrms_forward (one C-ABI call) captured once in a HIP graph, replayed per step"
+                        + (f"; {len(graphs)} batches in flight (--inflight: {len(graphs)} captured forwards, "
+                           "each with its own workspace, logits and stream, replayed in turn; every step "
+                           "still runs the whole forward of one batch)" if len(graphs) > 1 else ""))
                        if graph is not None else
                        "nrms_forward_timed without events (one C-ABI call per step)") if not args.unfused
                       else "ForwardPlan stage kernels (--unfused)",
