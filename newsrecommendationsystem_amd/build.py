@@ -27,9 +27,12 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, 
 # kernel ran 2.5 % faster under the iterative ILP scheduler until round 3;
 # since the token-compaction rewrite that scheduler spills ~45 registers
 # (scratch reloads inside the B epilogue) where the default spills 7 outside
-# the hot phases, so the news kernel takes the default.
+# the hot phases, so the news kernel took the default; after the round-4
+# pipeline changes max-ILP is 0.9 % faster end to end (news_fused -3.7 us,
+# 44 B of scratch per lane against 8; profiles/r4r2_news_sched_ab.txt).
 FILE_FLAGS = {
     "gemm_f32.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+    "news_fused.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
 }
 
 
