@@ -240,7 +240,8 @@ GEMM_CODES = {"f16x3": 2, "x6": 0, "f32": 1}   # nrms_gemm_arith_t
 
 
 def gemm_legs(model, cand, clk, mode, device, base, y_base):
-    """The timed step (nrms_forward, eager) under the other GEMM arithmetics:
+    """The timed step (nrms_forward, graph-replayed like the headline) under
+    the other GEMM arithmetics:
     ms / step, impressions / s, and the logits' distance to the default's
     (the CPU-port distance is added after the cpu_baseline leg)."""
     from newsrecommendationsystem_amd import _native as Nat
@@ -256,15 +257,39 @@ def gemm_legs(model, cand, clk, mode, device, base, y_base):
             f = TimedForward(model, B, C, N_CLICKED, L, proj_mode=mode)
             with torch.no_grad():
                 y = f.run(cand, clk).clone()
-                ms = _time_launches(lambda: f.run(cand, clk), 10, device)
+                eager = _time_launches(lambda: f.run(cand, clk), 10, device)
+                # the arithmetic switch is read at enqueue time: the captured
+                # graph replays this leg's kernels
+                gr = capture_graph(f, cand, clk, device)
+                f.logits.fill_(float("nan"))
+                gr.replay()
+                same = bool(torch.equal(f.logits, y))
+                ms = _time_launches(gr.replay, 20, device)
         finally:
             lib.nrms_set_gemm_arith(prev)
         legs[g] = {"ms_per_step": round(ms, 4), "impressions_per_s": round(B / (ms / 1e3), 1),
+                   "eager_ms_per_step": round(eager, 4), "graph_logits_equal_eager": same,
                    "max_normwise_rel_err_vs_default": float(
                        ((y - y_base).norm(dim=1) / y_base.norm(dim=1).clamp_min(1e-30)).max()),
-                   "timing": "eager nrms_forward calls, HIP events, 10 reps", "_logits": y}
-        del f
+                   "timing": "nrms_forward captured in a HIP graph and replayed (as the headline), HIP "
+                             "events over 20 replays; eager: 10 Python-issued calls",
+                   "_logits": y}
+        del gr, f
     return legs
+
+
+def capture_graph(f, cand, clk, device):
+    """f.run(cand, clk) captured into a HIP graph (one warm call on a side
+    stream first, as torch.cuda.graph requires)."""
+    side = torch.cuda.Stream(device)
+    side.wait_stream(torch.cuda.current_stream(device))
+    with torch.cuda.stream(side):
+        f.run(cand, clk)
+    torch.cuda.current_stream(device).wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        f.run(cand, clk)
+    return g
 
 
 def gather_hbm(device, V=1 << 20, n_titles=100_000, reps=20):
@@ -357,6 +382,12 @@ def issue_floor_ms(stage, w, gemm):
     return (gemm_s + rest_s) * 1e3
 
 
+def bytes_floor_ms(w):
+    """Time a stage's algorithmic bytes (what it must read and write,
+    pipeline.ForwardPlan.work) take at the 8 TB/s HBM peak."""
+    return w["bytes"] / (PEAK_HBM_GBS * 1e9) * 1e3
+
+
 def n_all_titles(B):
     return B * (C + N_CLICKED)
 
@@ -379,7 +410,13 @@ def main():
                     help="BASELINE cfg4: score the whole user-sharded 2M-impression stream once "
                          "(strong scaling; --steps is then the number of batches, 0 = all)")
     ap.add_argument("--stream-impressions", type=int, default=None)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true",
+                    help="skip the CPU-port leg (and the CPU-side AUC check and the FedAvg quality run)")
+    ap.add_argument("--no-quality", action="store_true",
+                    help="skip the reference-scale FedAvg quality run (quality.run_scaled, ~20 s)")
+    ap.add_argument("--as-shard", default=None, metavar="R/W",
+                    help="without a process group, take rank R of W's user shard of the stream (tests: a "
+                         "single-rank run of one shard of a multi-rank job)")
     ap.add_argument("--unfused", action="store_true", help="separate MHSA / additive / pool kernels")
     ap.add_argument("--no-extras", action="store_true", help="skip the gather / config-2 / direct figures")
     ap.add_argument("--no-graph", action="store_true", help="time the eager call loop instead of a HIP graph replay")
@@ -400,6 +437,8 @@ def main():
                     help="GEMM arithmetic: split-f16 news additive GEMM and Q|K|V projections "
                          "(default), split-bf16 x6 everywhere, or exact f32 MFMA (all fp32-accurate)")
     args = ap.parse_args()
+    if args.no_cpu_baseline:
+        args.no_quality = True
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -427,7 +466,12 @@ def main():
     B = args.batch
     # this rank's user shard of the config-4 stream (user_id % world); inputs
     # are generated into HBM before the timed region
-    idx = stream_impressions(rank, world, None if args.stream else B, device,
+    s_rank, s_world = rank, world
+    if args.as_shard:
+        if dist:
+            raise SystemExit("--as-shard is for single-process runs")
+        s_rank, s_world = (int(x) for x in args.as_shard.split("/"))
+    idx = stream_impressions(s_rank, s_world, None if args.stream else B, device,
                              n_impressions=args.stream_impressions)
     if args.stream:
         batches = [S.batch(0, idx[a:a + B], V_WORDS) for a in range(0, idx.numel(), B)]
@@ -480,14 +524,7 @@ def main():
             fwds = [fwd] + [TimedForward(model, B, C, N_CLICKED, L, proj_mode=mode)
                             for _ in range(max(1, args.inflight) - 1)]
             for f in fwds:
-                side = torch.cuda.Stream(device)
-                side.wait_stream(torch.cuda.current_stream(device))
-                with torch.cuda.stream(side):
-                    f.run(cand, clk)
-                torch.cuda.current_stream(device).wait_stream(side)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    f.run(cand, clk)
+                g = capture_graph(f, cand, clk, device)
                 f.logits.fill_(float("nan"))     # the replay must recompute them
                 g.replay()
                 torch.cuda.synchronize()
@@ -531,10 +568,18 @@ def main():
         elapsed = max_over_ranks(elapsed, device)
 
     if args.dump_logits:
-        # untimed: every batch of this rank's shard once, logits by impression index
+        # untimed: every batch of this rank's shard once, logits by impression
+        # index -- from the timed path itself (the captured graph's replay when
+        # the step is a graph replay: its logits buffer is poisoned first)
         import numpy as np
         with torch.no_grad():
-            ys = [fwd.run(*b).clone() for b in full] + ([tail_fwd.run(*tail[0]).clone()] if tail_fwd else [])
+            if graph is not None:
+                fwd.logits.fill_(float("nan"))
+                graph.replay()
+                torch.cuda.synchronize()
+                ys = [fwd.logits.clone()]
+            else:
+                ys = [fwd.run(*b).clone() for b in full] + ([tail_fwd.run(*tail[0]).clone()] if tail_fwd else [])
         n_done = sum(y.shape[0] for y in ys)
         np.savez(f"{args.dump_logits}.rank{rank}.npz", idx=idx[:n_done].cpu().numpy(),
                  logits=torch.cat(ys).float().cpu().numpy())
@@ -577,9 +622,16 @@ def main():
     dom = max(stage_ms, key=stage_ms.get)
     w = work[dom]
     t_dom = stage_ms[dom] / 1e3
-    intensity = w["flop"] / max(w["bytes"], 1)
-    if intensity >= PEAK_TFLOPS_F32 * 1e12 / (PEAK_HBM_GBS * 1e9):
-        achieved, peak, unit, bound = w["flop"] / t_dom / 1e12, PEAK_TFLOPS_F32, "TFLOP/s", "mfma"
+    floor = issue_floor_ms(dom, w, args.gemm)
+    bytes_floor = bytes_floor_ms(w)
+    # the binding floor: the larger of the instruction-issue floor (the
+    # matrix instructions the kernel actually issues, at their dense peaks)
+    # and the bytes floor (algorithmic bytes at 8 TB/s)
+    if floor is not None and floor > bytes_floor:
+        # peak = the kernel's algorithmic FLOP over its issue floor: the rate of
+        # its own instruction mix (split GEMM products at 2.5 PF, f32 at 157.3 TF)
+        achieved, peak, unit, bound = (w["flop"] / t_dom / 1e12, w["flop"] / (floor * 1e-3) / 1e12,
+                                       "TFLOP/s", "mfma")
     else:
         achieved, peak, unit, bound = w["bytes"] / t_dom / 1e9, PEAK_HBM_GBS, "GB/s", "hbm"
 
@@ -592,25 +644,39 @@ def main():
         value = done / elapsed
     else:
         value = world * B * steps / elapsed
-    floor = issue_floor_ms(dom, w, args.gemm)
-    # every stage's instruction-level floor and the fraction of it achieved
+    # every stage's floors (instruction issue, algorithmic bytes at 8 TB/s),
+    # the binding one and the fraction of it achieved; their sum is the step's
     stage_floor = {}
+    step_floor = 0.0
     for st_name, ms in stage_ms.items():
         if st_name in work:
             fl = issue_floor_ms(st_name, work[st_name], args.gemm)
-            if fl is not None:
-                stage_floor[st_name] = {"floor_ms": round(fl, 4), "frac": round(fl / ms, 4)}
+            bf = bytes_floor_ms(work[st_name])
+            bind = max(fl or 0.0, bf)
+            if ms > 0.002:   # (an empty event pair: stage folded into another launch)
+                step_floor += bind
+            stage_floor[st_name] = {"issue_floor_ms": None if fl is None else round(fl, 4),
+                                    "bytes_floor_ms": round(bf, 4),
+                                    "bound": "mfma" if (fl or 0.0) > bf else "hbm",
+                                    "floor_ms": round(bind, 4), "frac": round(bind / ms, 4) if ms > 0 else None}
     sq = load_sq(dom)
-    roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
-                "frac": round(achieved / peak, 4), "traffic": load_traffic(dom),
+    traffic = load_traffic(dom)
+    roofline = {"kernel": dom, "bound": bound, "achieved": round(achieved, 3), "peak": round(peak, 1), "unit": unit,
+                "frac": round(achieved / peak, 4), "traffic": traffic,
                 "algorithmic_per_launch": {"flop": w["flop"], "bytes": w["bytes"]},
-                "peak_note": "fp32 MFMA/vector peak; the split GEMMs issue 3 (f16x3) or 6 (x6) 16-bit "
-                             "products per fp32 product, so see issue_floor for the instruction-level "
-                             "ceiling"}
+                "bytes_floor_ms": round(bytes_floor, 4),
+                "peak_note": ("bound = the larger of the kernel's instruction-issue floor and its bytes floor "
+                              "(algorithmic bytes at 8 TB/s); frac = that floor / the measured launch time. "
+                              "hbm: achieved = algorithmic bytes / launch time. mfma: achieved = algorithmic "
+                              "fp32 FLOP / launch time, peak = those FLOP / the issue floor (the rate of the "
+                              "kernel's own instruction mix)"),
+                "fp32_flop_rate_vs_fp32_peak": round(w["flop"] / t_dom / 1e12 / PEAK_TFLOPS_F32, 4)}
+    if traffic:
+        roofline["traffic_vs_algorithmic"] = round(traffic / w["bytes"], 3)
     if floor is not None:
         # the fraction against the peak of the instructions the kernel actually
         # issues (its split GEMM's 16-bit products at 2.5 PF dense, the f32
-        # attention / pooling at 157.3 TF): how far it is from its own ceiling
+        # attention / pooling at 157.3 TF)
         roofline["frac_vs_issued_peak"] = round(floor / stage_ms[dom], 4)
         roofline["issue_floor"] = {
             "ms": round(floor, 4), "frac": round(floor / stage_ms[dom], 4),
@@ -659,10 +725,12 @@ def main():
                                  "no_token_compaction below)"},
         "stages_ms": {st: round(v, 4) for st, v in stage_ms.items()},
         "stages_issue_floor": stage_floor,
-        "stages_issue_floor_note": ("floor = the stage's algorithmic FLOP at the instruction rates it issues "
-                                    "(split GEMMs: their 16-bit products at 2.5 PF dense; attention / "
-                                    "pooling / exact f32 at 157.3 TF; the scorer: its bytes at 8 TB/s); "
-                                    "frac = floor / measured stage time"),
+        "stages_issue_floor_note": ("issue_floor = the stage's algorithmic FLOP at the instruction rates it "
+                                    "issues (split GEMMs: their 16-bit products at 2.5 PF dense; attention / "
+                                    "pooling / exact f32 at 157.3 TF); bytes_floor = its algorithmic bytes at "
+                                    "8 TB/s; floor = the larger (bound); frac = floor / measured stage time"),
+        "step_floor": {"ms": round(step_floor, 4), "frac_of_ms_per_step": round(step_floor / ms_per_step, 4),
+                       "note": "sum of the stages' binding floors against the timed step"},
         "user_rows_encoded": user_rows[0],
         "stages_note": f"HIP events recorded by the library between its stages, a separate pass of "
                        f"{n_ev} steps after the timed ones (events cost queue time, so the timed steps "
@@ -682,7 +750,11 @@ def main():
             "ms_per_step": round(eager_ms, 4), "impressions_per_s": round(B / (eager_ms / 1e3), 1),
             "note": "the same call issued from Python every step (no graph)"},
         "forward_paths_bitwise_equal": same,
+        "graph_replay": graph is not None,
+        "process_group": None if not dist else dist.get_backend(),
     }
+    if args.as_shard:
+        out["config"]["as_shard"] = args.as_shard
     if rank == 0 and world == 1 and not args.no_extras and not args.stream:
         out["gather_roofline"] = gather_hbm(device)
         out["news_encoder_cfg2"] = news_encoder_cfg2(model, device)
@@ -724,7 +796,7 @@ def main():
         # every operand split losslessly) beside the default's 22-bit operands
         legs = gemm_legs(model, cand, clk, mode, device, args.gemm, y_fwd)
         out["gemm_legs"] = legs
-    if rank == 0 and world == 1 and not args.no_extras and not args.stream:
+    if rank == 0 and world == 1 and not args.no_extras and not args.stream and not args.no_quality:
         # config 5's quality half (planted teacher, reference dimensions): FedAvg
         # on the HIP training path vs the reference op sequence + torch Adam,
         # both through evaluate()
@@ -741,8 +813,7 @@ def main():
         out["auc_vs_cpu"] = eval_auc_check(model, device)
     if rank == 0 and world == 1 and not args.no_extras and not args.stream:
         out["eval_throughput"] = eval_throughput(model, device)
-    else:
-        out["cpu_baseline"] = None
+    out.setdefault("cpu_baseline", None)
     for leg in legs.values():
         leg.pop("_logits", None)
     if rank == 0:
