@@ -1,5 +1,6 @@
 // Shared device helpers and launch plumbing for libnrms_hip.so (gfx950 only).
 #pragma once
+#include <cstdlib>
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -139,7 +140,17 @@ struct WeightRows {
 // same box, 2 reps each; 912 / 960: 0.877 / 0.906): the fused kernels' gathers
 // read the same 16-B slice offset from every row, and with every row on a
 // line boundary those slices all fall at one offset within the line.
-inline int64_t qkv_row_stride(int D) { return (int64_t)3 * D; }
+// NRMS_QKV_STRIDE (measurement only, profiles/r5): a larger stride spreads
+// the same rows over a larger address range (e.g. past the 256 MB Infinity
+// Cache) without changing the bytes any kernel reads or writes.
+inline int64_t qkv_row_stride(int D) {
+  static const int64_t extra = [] {
+    const char* e = getenv("NRMS_QKV_STRIDE");
+    return e ? (int64_t)atoll(e) - 900 : (int64_t)0;
+  }();
+  const int64_t s = (int64_t)3 * D;
+  return (extra > 0 && s == 900 && (s + extra) % 4 == 0) ? s + extra : s;
+}
 
 // Process-wide GEMM arithmetic (nrms_set_gemm_arith; defined in capi.hip).
 int gemm_arith();
