@@ -793,7 +793,8 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           // rows near fp32 overflow (or non-finite): flagged (no branch here),
           // recomputed by the EXACT pass (RecheckList)
           if constexpr (!EXACT) recheck |= __builtin_amdgcn_ballot_w64(exp_row_needs_recheck(sum));
-          const float inv = 1.0f / (sum + 1e-8f);
+          // (main pass: v_rcp_f32, 1 ulp; the recheck pass divides as the reference)
+          const float inv = EXACT ? 1.0f / (sum + 1e-8f) : __builtin_amdgcn_rcpf(sum + 1e-8f);
 #pragma unroll
           for (int j = 0; j < NB; ++j)
 #pragma unroll
@@ -1133,12 +1134,19 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           const int q = 4 * i + x;
           mult[i] = q < my_c ? 1.f : ((q == my_c && npad > 0) ? (float)npad : 0.f);
         }
+        // the softmax maximum over the counted rows (v_max_f32 skips a NaN) and
+        // nz = 0, or NaN when a counted score is NaN (scores are finite or NaN:
+        // sums of q tanh(.)); the quad's NaN is added to the maximum below, so
+        // a NaN score makes every weight of its title NaN, as F.softmax
+        float mx = -INFINITY, nz = 0.f;
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+          mx = mult[i] > 0.f ? fmaxf(mx, sc[i]) : mx;
+          nz = mult[i] > 0.f ? nz + (sc[i] - sc[i]) : nz;
+        }
         if constexpr (H3) {
           // a NaN score: an operand beyond fp16's range (or NaN inputs) -> recheck pass
-          bool bad = false;
-#pragma unroll
-          for (int i = 0; i < NB; ++i) bad |= mult[i] > 0.f && sc[i] != sc[i];
-          recheck |= __builtin_amdgcn_ballot_w64(bad);
+          recheck |= __builtin_amdgcn_ballot_w64(nz != nz);
         }
         if constexpr (!EXACT) {
           // titles of the flagged lanes (title at = lanes 16 at .. 16 at + 15)
@@ -1147,11 +1155,11 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           for (int t = 0; t < FT; ++t) tm |= ((recheck >> (16 * t)) & 0xFFFFull) ? (1 << t) : 0;
           if (tm != 0 && lane == 0) rl.list[atomicAdd(rl.count, 1)] = (int32_t)((k << 4) | tm);
         }
-        float mx = -INFINITY;
-#pragma unroll
-        for (int i = 0; i < NB; ++i) mx = mult[i] > 0.f ? nan_max(mx, sc[i]) : mx;
-        mx = nan_max(mx, quad_xor1(mx));
-        mx = nan_max(mx, quad_xor2(mx));
+        mx = fmaxf(mx, quad_xor1(mx));
+        nz += quad_xor1(nz);
+        mx = fmaxf(mx, quad_xor2(mx));
+        nz += quad_xor2(nz);
+        mx += nz;
         // exp on v_exp_f32 (arguments <= 0: no overflow; NaN propagates) and one
         // reciprocal per title instead of a division per row (fp32 rounding)
         float ex[NB], sum = 0.f;
