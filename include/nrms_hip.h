@@ -56,7 +56,7 @@ extern "C" {
 /* 7: host-side readers of the eval split files (nrms_behaviors_scan /
  *    nrms_behaviors_parse / nrms_news_parse); nrms_forward's workspace holds
  *    the UserEncoder dispatch order (nrms_forward_workspace_size grew). */
-#define NRMS_ABI_VERSION 7
+#define NRMS_ABI_VERSION 8
 
 typedef enum {
   NRMS_OK = 0,
@@ -411,10 +411,21 @@ int32_t nrms_score_backward(const float* news, int64_t B, int32_t C, int64_t str
 
 /* Backward of nrms_embedding_gather as nn.Embedding(padding_idx) computes it:
  * dtable[ids[t]] += dx[t] for every t with ids[t] != padding_idx (dense
- * [V, D] gradient, accumulated). */
+ * [V, D] gradient, accumulated). Float atomics: the additions to one row land
+ * in arrival order, so results may differ by rounding from run to run; the _ws
+ * form below is deterministic. */
 int32_t nrms_embedding_backward(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
                                 int32_t D, int64_t padding_idx, float* dtable,
                                 hipStream_t stream);
+
+/* (ABI 8) The same gradient, deterministic: the tokens are sorted by id (a
+ * stable radix sort) and each row's contributions added in token order, the
+ * order of the CPU reference's index_add; bitwise reproducible. Workspace:
+ * nrms_embedding_backward_workspace_size(n_tok, V) bytes; n_tok, V < 2^31. */
+size_t nrms_embedding_backward_workspace_size(int64_t n_tok, int64_t V);
+int32_t nrms_embedding_backward_ws(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
+                                   int32_t D, int64_t padding_idx, float* dtable, void* workspace,
+                                   size_t workspace_bytes, hipStream_t stream);
 
 /* torch.optim.Adam step (src/train.py:127; amsgrad off, no weight decay) on
  * one parameter, in torch's operation order; `step` counts from 1. */

@@ -12,7 +12,7 @@ import torch  # noqa: F401  (must precede the CDLL load: shared HIP runtime)
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NRMS_LIB_PATH") or os.path.join(_PKG, "libnrms_hip.so")   # override: A/B builds
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 NRMS_PROJ_AUTO, NRMS_PROJ_DIRECT, NRMS_PROJ_FOLDED = 0, 1, 2
 NRMS_GEMM_SPLIT_BF16X6, NRMS_GEMM_F32, NRMS_GEMM_SPLIT_F16X3 = 0, 1, 2
@@ -81,6 +81,8 @@ SIGNATURES = {
     "nrms_qkv_project_backward": (_i32, [_p, _i64, _EW, _p, _p, _p, _p, _p, _sz, _p]),
     "nrms_score_backward": (_i32, [_p, _i64, _i32, _i64, _i64, _p, _i64, _i32, _p, _p, _p, _p]),
     "nrms_embedding_backward": (_i32, [_p, _i64, _p, _i64, _i32, _i64, _p, _p]),
+    "nrms_embedding_backward_workspace_size": (_sz, [_i64, _i64]),
+    "nrms_embedding_backward_ws": (_i32, [_p, _i64, _p, _i64, _i32, _i64, _p, _p, _sz, _p]),
     "nrms_adam_step": (_i32, [_p, _p, _p, _p, _i64, ctypes.c_float, ctypes.c_float, ctypes.c_float,
                               ctypes.c_float, _i64, _p]),
     "nrms_adam_step_multi": (_i32, [_p, _i32, ctypes.c_float, ctypes.c_float, ctypes.c_float,

@@ -17,7 +17,7 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 OBJ = os.path.join(PKG, "_build")
 LIB = os.path.join(PKG, "libnrms_hip.so")
-SOURCES = ["gather.hip", "gemm_f32.hip", "proj_x6.hip", "attention.hip", "news_fused.hip", "user_fused.hip", "score.hip", "eval.hip", "train.hip", "tsv_io.hip", "capi.hip"]
+SOURCES = ["gather.hip", "gemm_f32.hip", "proj_x6.hip", "attention.hip", "news_fused.hip", "user_fused.hip", "score.hip", "eval.hip", "train.hip", "embed_sort.hip", "tsv_io.hip", "capi.hip"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,

@@ -716,7 +716,8 @@ int32_t nrms_additive_forward_train(const float* x, int64_t n_seq, int32_t L,
 
 size_t nrms_additive_backward_workspace_size(int64_t n_seq, int32_t L, int32_t D, int32_t Q) {
   if (n_seq < 0 || L <= 0 || D <= 0 || Q <= 0) return 0;
-  return align_up((size_t)n_seq * L * Q * 4) + align_up((size_t)D * Q * 4);
+  return align_up((size_t)n_seq * L * Q * 4) + align_up((size_t)D * Q * 4) +
+         align_up(additive_backward_part_floats(n_seq, Q) * 4) + align_up(gemm_tn_part_floats(Q, D) * 4);
 }
 
 int32_t nrms_additive_backward(const float* x, int64_t n_seq, int32_t L,
@@ -734,9 +735,11 @@ int32_t nrms_additive_backward(const float* x, int64_t n_seq, int32_t L,
   Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
   float* dz = cv.floats((size_t)n_seq * L * Q);
   float* waT = cv.floats((size_t)D * Q);
+  float* part_rows = cv.floats(additive_backward_part_floats(n_seq, Q));
+  float* part_tn = cv.floats(gemm_tn_part_floats(Q, D));
   if (!cv.ok) return NRMS_ERR_WORKSPACE;
   int32_t st = launch_additive_backward_rows(x, y_tanh, scores, w->q_add, dout, n_seq, L, D, Q, dx,
-                                             dz, d_q_add, d_b_add, stream);
+                                             dz, d_q_add, d_b_add, part_rows, stream);
   if (st) return st;
   const float* wa[1] = {w->w_add};
   st = launch_transpose(wa, 1, Q, D, waT, stream);   // [Q, D] -> [D, Q]
@@ -749,7 +752,7 @@ int32_t nrms_additive_backward(const float* x, int64_t n_seq, int32_t L,
   r.accumulate = 1;
   st = launch_gemm_store_f32(dz, n_seq * L, Q, r, D, dx, D, stream);   // dx += dz W_add
   if (st) return st;
-  return launch_gemm_tn(dz, n_seq * L, Q, x, D, d_w_add, nullptr, stream);   // dW += dz^T x
+  return launch_gemm_tn(dz, n_seq * L, Q, x, D, d_w_add, nullptr, part_tn, stream);   // dW += dz^T x
 }
 
 int32_t nrms_self_attention_backward(const float* qkv, const float* dctx, int64_t n_seq,
@@ -764,7 +767,7 @@ int32_t nrms_self_attention_backward(const float* qkv, const float* dctx, int64_
 
 size_t nrms_qkv_project_backward_workspace_size(int32_t D) {
   if (D <= 0) return 0;
-  return align_up((size_t)3 * D * D * 4);
+  return align_up((size_t)3 * D * D * 4) + align_up(gemm_tn_part_floats(3 * D, D) * 4);
 }
 
 int32_t nrms_qkv_project_backward(const float* x, int64_t rows, const nrms_encoder_weights_t* w,
@@ -776,10 +779,11 @@ int32_t nrms_qkv_project_backward(const float* x, int64_t rows, const nrms_encod
   if (!x || !dqkv || !d_w_qkv || !d_b_qkv) return NRMS_ERR_INVALID_ARG;
   const int D = w->d_model;
   int32_t st;
+  Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
+  float* wT = cv.floats((size_t)3 * D * D);
+  float* part_tn = cv.floats(gemm_tn_part_floats(3 * D, D));
+  if (!cv.ok) return NRMS_ERR_WORKSPACE;
   if (dx) {
-    Carve cv{static_cast<char*>(workspace), workspace ? workspace_bytes : 0};
-    float* wT = cv.floats((size_t)3 * D * D);
-    if (!cv.ok) return NRMS_ERR_WORKSPACE;
     const float* ws3[3] = {w->w_q, w->w_k, w->w_v};
     st = launch_transpose(ws3, 3, D, D, wT, stream);   // [3D, D] -> [D, 3D]
     if (st) return st;
@@ -791,7 +795,7 @@ int32_t nrms_qkv_project_backward(const float* x, int64_t rows, const nrms_encod
     st = launch_gemm_store_f32(dqkv, rows, 3 * D, r, D, dx, D, stream);   // dx = dqkv [Wq; Wk; Wv]
     if (st) return st;
   }
-  return launch_gemm_tn(dqkv, rows, 3 * D, x, D, d_w_qkv, d_b_qkv, stream);
+  return launch_gemm_tn(dqkv, rows, 3 * D, x, D, d_w_qkv, d_b_qkv, part_tn, stream);
 }
 
 int32_t nrms_score_backward(const float* news, int64_t B, int32_t C, int64_t stride_b,
@@ -809,6 +813,20 @@ int32_t nrms_embedding_backward(const int64_t* ids, int64_t n_tok, const float* 
   if (n_tok < 0 || V <= 0 || D <= 0) return NRMS_ERR_INVALID_ARG;
   if (n_tok > 0 && (!ids || !dx || !dtable)) return NRMS_ERR_INVALID_ARG;
   return launch_embedding_backward(ids, n_tok, dx, V, D, padding_idx, dtable, stream);
+}
+
+size_t nrms_embedding_backward_workspace_size(int64_t n_tok, int64_t V) {
+  if (n_tok < 0 || V <= 0) return 0;
+  return embedding_backward_sorted_bytes(n_tok, V);
+}
+
+int32_t nrms_embedding_backward_ws(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V, int32_t D,
+                                   int64_t padding_idx, float* dtable, void* workspace, size_t workspace_bytes,
+                                   hipStream_t stream) {
+  if (n_tok < 0 || V <= 0 || D <= 0) return NRMS_ERR_INVALID_ARG;
+  if (n_tok > 0 && (!ids || !dx || !dtable)) return NRMS_ERR_INVALID_ARG;
+  return launch_embedding_backward_sorted(ids, n_tok, dx, V, D, padding_idx, dtable, workspace, workspace_bytes,
+                                          stream);
 }
 
 int32_t nrms_adam_step(float* param, const float* grad, float* exp_avg, float* exp_avg_sq,

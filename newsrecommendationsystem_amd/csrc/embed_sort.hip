@@ -1,0 +1,115 @@
+// Deterministic embedding backward (nn.Embedding(padding_idx) backward,
+// src/model/NRMS/news_encoder.py:14-20,38): dtable[id] += dx[t] for every
+// token t with ids[t] != padding_idx, summed per id in token order -- the
+// order of the CPU reference's index_add -- so two runs give bitwise the same
+// gradient (the atomic form in train.hip adds in arrival order).
+//
+//   keys:  key[t] = ids[t], or V for padding / out-of-range ids (sorted last)
+//   sort:  (key, t) pairs by key, stable LSD radix sort (rocPRIM via hipCUB):
+//          within one id the tokens stay in ascending t
+//   sum:   one wave per sorted position that starts a run of equal keys:
+//          acc = dtable[id]; acc += dx[t] for the run's tokens in order; store
+#include "nrms_common.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+namespace nrms {
+namespace {
+
+__global__ __launch_bounds__(256) void embed_keys_kernel(const int64_t* __restrict__ ids, int64_t n, int64_t V,
+                                                         int64_t padding_idx, int32_t* __restrict__ key,
+                                                         int32_t* __restrict__ tok) {
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= n) return;
+  const int64_t id = ids[t];
+  key[t] = (id == padding_idx || (uint64_t)id >= (uint64_t)V) ? (int32_t)V : (int32_t)id;
+  tok[t] = (int32_t)t;
+}
+
+// one wave per sorted position i; only the first position of each run of
+// equal keys works (the others exit at once)
+__global__ __launch_bounds__(256) void embed_run_sum_kernel(const int32_t* __restrict__ key,
+                                                            const int32_t* __restrict__ tok, int64_t n,
+                                                            int64_t V, const float* __restrict__ dx, int D,
+                                                            float* __restrict__ dtable) {
+  const int lane = threadIdx.x & 63;
+  const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int32_t k = key[i];
+  if (k >= V || (i > 0 && key[i - 1] == k)) return;
+  float* row = dtable + (int64_t)k * D;
+  for (int d0 = 0; d0 < D; d0 += 64 * 4) {
+    float acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = d0 + lane + 64 * j;
+      acc[j] = d < D ? row[d] : 0.f;
+    }
+    for (int64_t p = i; p < n && key[p] == k; ++p) {
+      const float* src = dx + (int64_t)tok[p] * D;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = d0 + lane + 64 * j;
+        if (d < D) acc[j] += src[d];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int d = d0 + lane + 64 * j;
+      if (d < D) row[d] = acc[j];
+    }
+  }
+}
+
+int end_bit_of(int64_t V) {
+  int b = 1;
+  while (b < 31 && ((int64_t)1 << b) <= V) ++b;   // keys 0..V fit in b bits
+  return b;
+}
+
+size_t sort_temp_bytes(int64_t n, int64_t V) {
+  size_t bytes = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, end_bit_of(V),
+                                           (hipStream_t)0);
+  return bytes;
+}
+
+constexpr size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+}  // namespace
+
+size_t embedding_backward_sorted_bytes(int64_t n_tok, int64_t V) {
+  if (n_tok <= 0 || n_tok > INT32_MAX || V <= 0 || V >= INT32_MAX) return 0;
+  return 4 * align256((size_t)n_tok * 4) + align256(sort_temp_bytes(n_tok, V));
+}
+
+int32_t launch_embedding_backward_sorted(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V, int D,
+                                         int64_t padding_idx, float* dtable, void* ws, size_t ws_bytes,
+                                         hipStream_t s) {
+  if (n_tok == 0) return NRMS_OK;
+  if (n_tok > INT32_MAX || V >= INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  if (!ws || ws_bytes < embedding_backward_sorted_bytes(n_tok, V)) return NRMS_ERR_WORKSPACE;
+  char* p = static_cast<char*>(ws);
+  const size_t a = align256((size_t)n_tok * 4);
+  int32_t* key_in = reinterpret_cast<int32_t*>(p);
+  int32_t* tok_in = reinterpret_cast<int32_t*>(p + a);
+  int32_t* key_out = reinterpret_cast<int32_t*>(p + 2 * a);
+  int32_t* tok_out = reinterpret_cast<int32_t*>(p + 3 * a);
+  void* temp = p + 4 * a;
+  size_t temp_bytes = ws_bytes - 4 * a;
+  hipLaunchKernelGGL(embed_keys_kernel, dim3((unsigned)((n_tok + 255) / 256)), dim3(256), 0, s, ids, n_tok, V,
+                     padding_idx, key_in, tok_in);
+  if (int32_t st = launch_status()) return st;
+  const hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, key_in, key_out, tok_in, tok_out,
+                                                          (int)n_tok, 0, end_bit_of(V), s);
+  if (e != hipSuccess) {
+    set_last_hip_error(e);
+    return NRMS_ERR_HIP;
+  }
+  hipLaunchKernelGGL(embed_run_sum_kernel, dim3((unsigned)((n_tok + 3) / 4)), dim3(256), 0, s, key_out, tok_out,
+                     n_tok, V, dx, D, dtable);
+  return launch_status();
+}
+
+}  // namespace nrms

@@ -235,18 +235,30 @@ int32_t launch_dropout(const float* x, float* y, int64_t n, float p, uint64_t se
 int32_t launch_score_backward(const float* news, int64_t B, int C, int64_t sb, int64_t sc,
                               const float* user, int64_t su, int D, const float* dl, float* dnews,
                               float* duser, hipStream_t s);
+// (deterministic: per-sequence dq / db partials in `part` [2][n_seq][Q], then a
+// fixed-order reduction into dq, db)
 int32_t launch_additive_backward_rows(const float* x, const float* y, const float* score,
                                       const float* q, const float* dout, int64_t n_seq, int L,
                                       int D, int Q, float* dx, float* dz, float* dq, float* db,
-                                      hipStream_t s);
+                                      float* part, hipStream_t s);
+size_t additive_backward_part_floats(int64_t n_seq, int Q);
 int32_t launch_mhsa_backward(const float* qkv, const float* dctx, int64_t n_seq, int L, int D,
                              int H, float* dqkv, hipStream_t s);
+// dW += dY^T X (+ db += column sums of dY), deterministic: row-slice partials
+// in `part` (gemm_tn_part_floats(N, K) floats), summed in slice order.
 int32_t launch_gemm_tn(const float* dY, int64_t R, int N, const float* X, int K, float* dW,
-                       float* db, hipStream_t s);
+                       float* db, float* part, hipStream_t s);
+size_t gemm_tn_part_floats(int N, int K);
 int32_t launch_transpose(const float* const* src, int nseg, int seg_rows, int cols, float* dst,
                          hipStream_t s);
 int32_t launch_embedding_backward(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
                                   int D, int64_t padding_idx, float* dtable, hipStream_t s);
+// The same, deterministic: tokens sorted by id (stable radix sort: token order
+// within an id), one wave per id summing its rows in token order.
+size_t embedding_backward_sorted_bytes(int64_t n_tok, int64_t V);
+int32_t launch_embedding_backward_sorted(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,
+                                         int D, int64_t padding_idx, float* dtable, void* ws,
+                                         size_t ws_bytes, hipStream_t s);
 int32_t launch_adam_multi(const nrms_adam_tensor_t* ts, int n, float lr, float b1, float b2,
                           float eps, int64_t step, hipStream_t s);
 int32_t launch_adam(float* p, const float* g, float* m, float* v, int64_t n, float lr, float b1,

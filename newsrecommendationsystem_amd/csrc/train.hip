@@ -11,8 +11,12 @@
 //   additive_backward  softmax / tanh·q chain per sequence; dz = ds q (1 - y^2)
 //   mhsa_backward      raw-exp attention per (sequence, head): A = E / (Z + 1e-8),
 //                      dS = A (dA - rowsum(dA A)), dQ = dS K / sqrt(dk), ...
-//   gemm_tn            dW[n][k] += sum_r dY[r][n] X[r][k] (split over rows, atomics)
-//   embedding_backward dtable[id] += dx (rows with id == padding_idx skipped)
+//   gemm_tn            dW[n][k] += sum_r dY[r][n] X[r][k] (split over row slices; the
+//                      slices' partials summed in slice order: deterministic)
+//   embedding_backward dtable[id] += dx (rows with id == padding_idx skipped);
+//                      deterministic form: tokens sorted by id (embed_sort.hip)
+// Every training kernel is deterministic (no float atomics): two runs of a step
+// give bitwise the same gradients (tests/test_gpu_train.py).
 //   adam               torch.optim.Adam's update, same operation order
 #include "nrms_common.hpp"
 
@@ -63,12 +67,13 @@ __global__ __launch_bounds__(256) void score_backward_kernel(
 //   dw_l   = x_l · dout
 //   ds_l   = w_l (dw_l - sum_l' w_l' dw_l')
 //   dz_lq  = ds_l q_q (1 - y_lq^2)       (written, [rows, Q])
-//   dq    += sum_l ds_l y_l ;  db += sum_l dz_l   (atomics, one per column per sequence)
+//   dq    += sum_l ds_l y_l ;  db += sum_l dz_l   (per-sequence partials pq / pb
+//            [n_seq][Q], summed over the sequences in a fixed order by reduce_rows_add)
 __global__ __launch_bounds__(256) void additive_backward_rows_kernel(
     const float* __restrict__ x, const float* __restrict__ y, const float* __restrict__ score,
     const float* __restrict__ q, const float* __restrict__ dout, int L, int D, int Q,
-    float* __restrict__ dx, float* __restrict__ dz, float* __restrict__ dq,
-    float* __restrict__ db) {
+    float* __restrict__ dx, float* __restrict__ dz, float* __restrict__ pq,
+    float* __restrict__ pb) {
   __shared__ float sw[64], sds[64], sdw[64];
   const int64_t s = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -109,9 +114,55 @@ __global__ __launch_bounds__(256) void additive_backward_rows_kernel(
       aq = fmaf(sds[l], yv, aq);
       ab += g;
     }
-    atomicAdd(dq + qq, aq);
-    atomicAdd(db + qq, ab);
+    pq[s * Q + qq] = aq;
+    pb[s * Q + qq] = ab;
   }
+}
+
+// Column sums of part [rows][cols] in a fixed order (deterministic): thread
+// (column c, chunk blockIdx.y) sums rows [chunk y, chunk (y + 1)) in order
+// (loads eight rows ahead); with one chunk the sum is added to out[c],
+// otherwise stored to out[y][c] for a second pass.
+__global__ __launch_bounds__(256) void reduce_rows_kernel(const float* __restrict__ part, int64_t rows,
+                                                          int64_t cols, int64_t chunk, float* __restrict__ out,
+                                                          int accumulate) {
+  const int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int64_t r0 = (int64_t)blockIdx.y * chunk, r1 = r0 + chunk < rows ? r0 + chunk : rows;
+  float a = 0.f;
+  int64_t r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    float v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = part[(r + i) * cols + c];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a += v[i];
+  }
+  for (; r < r1; ++r) a += part[r * cols + c];
+  if (accumulate) out[c] += a;
+  else out[(int64_t)blockIdx.y * cols + c] = a;
+}
+
+constexpr int64_t RED_CHUNK = 64;
+// floats of the second-pass buffer reduce_rows_add needs for `rows` rows
+inline size_t reduce_scratch_floats(int64_t rows, int64_t cols) {
+  return rows > RED_CHUNK ? (size_t)((rows + RED_CHUNK - 1) / RED_CHUNK) * cols : 0;
+}
+// out[c] += sum_r part[r][c]: one pass for at most RED_CHUNK rows, else chunks
+// of RED_CHUNK rows into `scratch` and a second pass over the chunk sums
+int32_t reduce_rows_add(const float* part, int64_t rows, int64_t cols, float* out, float* scratch, hipStream_t s) {
+  const unsigned gx = (unsigned)((cols + 255) / 256);
+  if (rows <= RED_CHUNK) {
+    hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx), dim3(256), 0, s, part, rows, cols, rows, out, 1);
+    return launch_status();
+  }
+  const int64_t nch = (rows + RED_CHUNK - 1) / RED_CHUNK;
+  if (nch > 65535) return NRMS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx, (unsigned)nch), dim3(256), 0, s, part, rows, cols, RED_CHUNK,
+                     scratch, 0);
+  if (int32_t st = launch_status()) return st;
+  hipLaunchKernelGGL(reduce_rows_kernel, dim3(gx), dim3(256), 0, s, scratch, nch, cols, nch, out, 1);
+  return launch_status();
 }
 
 // Raw-exp multi-head attention backward, one workgroup per (sequence, head).
@@ -282,25 +333,34 @@ __global__ __launch_bounds__(256) void mhsa_backward_wave_kernel(const float* __
   }
 }
 
-// dW[n][k] += sum_r dY[r][n] X[r][k] (+ db[n] += sum_r dY[r][n] from the
-// column tile 0 blocks). f32 MFMA 16x16x4; block = 64 (n) x 64 (k) tile over a
-// 256-row slice, 4 waves each a 16-row (n) strip x 64 cols; LDS tiles of
-// 32 rows; the slice's partial sums go to global with atomics.
-constexpr int TN_TILE = 64, TN_ROWS = 256, TN_BK = 32;
+// part[z][n][k] = sum_{r in slice z} dY[r][n] X[r][k] (+ part_b[z][n] = the
+// slice's column sums of dY, from the column tile 0 blocks). f32 MFMA 16x16x4;
+// block = 64 (n) x 64 (k) tile over a row slice of `slice` rows (a multiple
+// of 32), 4 waves each a 16-row (n) strip x 64 cols; LDS tiles of 32 rows.
+// The slices' partials are summed in slice order (reduce_rows_add).
+constexpr int TN_TILE = 64, TN_BK = 32;
+#ifndef NRMS_TN_BLOCKS
+#define NRMS_TN_BLOCKS 4096
+#endif
+#ifndef NRMS_TN_MAX_SLICES
+#define NRMS_TN_MAX_SLICES 64
+#endif
+constexpr int TN_BLOCKS = NRMS_TN_BLOCKS;    // aim: (n tiles) x (k tiles) x slices >= this many blocks
+constexpr int TN_MAX_SLICES = NRMS_TN_MAX_SLICES;
 __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ dY, int64_t R,
                                                       int N, const float* __restrict__ X, int K,
-                                                      float* __restrict__ dW,
-                                                      float* __restrict__ db) {
+                                                      int64_t slice, float* __restrict__ part,
+                                                      float* __restrict__ part_b) {
   __shared__ float sy[TN_BK][TN_TILE + 1], sx[TN_BK][TN_TILE + 1];
   const int n0 = blockIdx.x * TN_TILE, k0 = blockIdx.y * TN_TILE;
-  const int64_t r0 = (int64_t)blockIdx.z * TN_ROWS;
+  const int64_t r0 = (int64_t)blockIdx.z * slice;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lm = lane & 15, kq = lane >> 4;
   floatx4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = floatx4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f;   // db: thread tid < 64 sums column n0 + tid
-  for (int rb = 0; rb < TN_ROWS; rb += TN_BK) {
+  for (int64_t rb = 0; rb < slice && r0 + rb < R; rb += TN_BK) {
     for (int e = tid; e < TN_BK * TN_TILE; e += 256) {
       const int rr = e / TN_TILE, c = e - rr * TN_TILE;
       const int64_t r = r0 + rb + rr;
@@ -309,7 +369,7 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ 
       sx[rr][c] = (rin && k0 + c < K) ? X[r * K + k0 + c] : 0.f;
     }
     __syncthreads();
-    if (db && blockIdx.y == 0 && tid < TN_TILE)
+    if (part_b && blockIdx.y == 0 && tid < TN_TILE)
       for (int rr = 0; rr < TN_BK; ++rr) bsum += sy[rr][tid];
 #pragma unroll
     for (int kk = 0; kk < TN_BK; kk += 4) {
@@ -329,9 +389,9 @@ __global__ __launch_bounds__(256) void gemm_tn_kernel(const float* __restrict__ 
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + 16 * w + 4 * kq + r, k = k0 + 16 * j + lm;
-      if (n < N && k < K) atomicAdd(dW + (int64_t)n * K + k, acc[j][r]);
+      if (n < N && k < K) part[((int64_t)blockIdx.z * N + n) * K + k] = acc[j][r];
     }
-  if (db && blockIdx.y == 0 && tid < TN_TILE && n0 + tid < N) atomicAdd(db + n0 + tid, bsum);
+  if (part_b && blockIdx.y == 0 && tid < TN_TILE && n0 + tid < N) part_b[(int64_t)blockIdx.z * N + n0 + tid] = bsum;
 }
 
 // The same dW += dY^T X on split-bf16 x6 (v_mfma_f32_16x16x32_bf16, the
@@ -346,12 +406,12 @@ __device__ __forceinline__ int tn_xsw(int row) { return ((row >> 3) & 1) << 1; }
 
 __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(const float* __restrict__ dY, int64_t R,
                                                          int N, const float* __restrict__ X, int K,
-                                                         float* __restrict__ dW,
-                                                         float* __restrict__ db) {
+                                                         int64_t slice, float* __restrict__ part,
+                                                         float* __restrict__ part_b) {
   constexpr int RK = 32, PL = TN_TILE * RK;   // rows per chunk, bf16 per plane
   __shared__ __attribute__((aligned(16))) __bf16 sa[3 * PL], sb[3 * PL];
   const int n0 = blockIdx.x * TN_TILE, k0 = blockIdx.y * TN_TILE;
-  const int64_t r0 = (int64_t)blockIdx.z * TN_ROWS;
+  const int64_t r0 = (int64_t)blockIdx.z * slice;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lm = lane & 15, kq = lane >> 4;
   // staging role: a 4 x 4 block (rows 4 rb.., columns 4 cb..) of dY or X
@@ -398,8 +458,8 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(const float* __restrict
   gload(r0);
   stage();
   __syncthreads();
-  for (int rc = 0; rc < TN_ROWS; rc += RK) {
-    const bool more = rc + RK < TN_ROWS && r0 + rc + RK < R;
+  for (int64_t rc = 0; rc < slice; rc += RK) {
+    const bool more = rc + RK < slice && r0 + rc + RK < R;
     if (more) gload(r0 + rc + RK);
     tn_bf16x8 a[3];
 #pragma unroll
@@ -428,9 +488,9 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(const float* __restrict
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + 16 * w + 4 * kq + r, k = k0 + 16 * j + lm;
-      if (n < N && k < K) atomicAdd(dW + (int64_t)n * K + k, acc[j][r]);
+      if (n < N && k < K) part[((int64_t)blockIdx.z * N + n) * K + k] = acc[j][r];
     }
-  if (db && blockIdx.y == 0) {
+  if (part_b && blockIdx.y == 0) {
     // the slice's rows are spread over the 8 rb threads of a column block:
     // combine their partials through LDS (the staging tiles are free now)
     __syncthreads();
@@ -443,7 +503,7 @@ __global__ __launch_bounds__(256) void gemm_tn_x6_kernel(const float* __restrict
       float sum = 0.f;
 #pragma unroll
       for (int q = 0; q < 8; ++q) sum += red[q * TN_TILE + tid];
-      atomicAdd(db + n0 + tid, sum);
+      part_b[(int64_t)blockIdx.z * N + n0 + tid] = sum;
     }
   }
 }
@@ -552,15 +612,25 @@ int32_t launch_score_backward(const float* news, int64_t B, int C, int64_t sb, i
   return launch_status();
 }
 
+size_t additive_backward_part_floats(int64_t n_seq, int Q) {
+  return (size_t)2 * n_seq * Q + 2 * reduce_scratch_floats(n_seq, Q);
+}
+
 int32_t launch_additive_backward_rows(const float* x, const float* y, const float* score,
                                       const float* q, const float* dout, int64_t n_seq, int L,
                                       int D, int Q, float* dx, float* dz, float* dq, float* db,
-                                      hipStream_t s) {
+                                      float* part, hipStream_t s) {
   if (n_seq == 0) return NRMS_OK;
   if (L < 1 || L > 64) return NRMS_ERR_UNSUPPORTED;
+  if (n_seq > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  float* pq = part;
+  float* pb = part + n_seq * Q;
   hipLaunchKernelGGL(additive_backward_rows_kernel, dim3((unsigned)n_seq), dim3(256), 0, s, x, y,
-                     score, q, dout, L, D, Q, dx, dz, dq, db);
-  return launch_status();
+                     score, q, dout, L, D, Q, dx, dz, pq, pb);
+  if (int32_t st = launch_status()) return st;
+  float* scratch = pb + n_seq * Q;
+  if (int32_t st = reduce_rows_add(pq, n_seq, Q, dq, scratch, s)) return st;
+  return reduce_rows_add(pb, n_seq, Q, db, scratch + reduce_scratch_floats(n_seq, Q), s);
 }
 
 int32_t launch_mhsa_backward(const float* qkv, const float* dctx, int64_t n_seq, int L, int D,
@@ -578,19 +648,39 @@ int32_t launch_mhsa_backward(const float* qkv, const float* dctx, int64_t n_seq,
   return launch_status();
 }
 
+// row slices of dW += dY^T X: enough blocks to fill the chip, at most
+// TN_MAX_SLICES (the partials' workspace does not grow with R)
+static int64_t gemm_tn_slices(int N, int K) {
+  const int64_t tiles = (int64_t)((N + TN_TILE - 1) / TN_TILE) * ((K + TN_TILE - 1) / TN_TILE);
+  const int64_t z = (TN_BLOCKS + tiles - 1) / tiles;
+  return z < 1 ? 1 : (z > TN_MAX_SLICES ? TN_MAX_SLICES : z);
+}
+size_t gemm_tn_part_floats(int N, int K) {
+  const int64_t z = gemm_tn_slices(N, K), nk = (int64_t)N * K;
+  return (size_t)z * (nk + N) + reduce_scratch_floats(z, nk) + reduce_scratch_floats(z, N);
+}
+
 int32_t launch_gemm_tn(const float* dY, int64_t R, int N, const float* X, int K, float* dW,
-                       float* db, hipStream_t s) {
+                       float* db, float* part, hipStream_t s) {
   if (R == 0) return NRMS_OK;
-  const int64_t zs = (R + TN_ROWS - 1) / TN_ROWS;
-  if (zs > 65535) return NRMS_ERR_UNSUPPORTED;
+  if (!part) return NRMS_ERR_WORKSPACE;
+  // slices of a multiple of 32 rows; zs <= gemm_tn_slices(N, K)
+  int64_t slice = (R + gemm_tn_slices(N, K) - 1) / gemm_tn_slices(N, K);
+  slice = (slice + TN_BK - 1) / TN_BK * TN_BK;
+  const int64_t zs = (R + slice - 1) / slice;
   dim3 grid((N + TN_TILE - 1) / TN_TILE, (K + TN_TILE - 1) / TN_TILE, (unsigned)zs);
+  float* part_b = db ? part + zs * (int64_t)N * K : nullptr;
   const bool x6 = gemm_arith() != NRMS_GEMM_F32 && N % 4 == 0 && K % 4 == 0 &&
                   ((uintptr_t)dY | (uintptr_t)X) % 16 == 0;
   if (x6)
-    hipLaunchKernelGGL(gemm_tn_x6_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, dW, db);
+    hipLaunchKernelGGL(gemm_tn_x6_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, slice, part, part_b);
   else
-    hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, dW, db);
-  return launch_status();
+    hipLaunchKernelGGL(gemm_tn_kernel, grid, dim3(256), 0, s, dY, R, N, X, K, slice, part, part_b);
+  if (int32_t st = launch_status()) return st;
+  const int64_t zmax = gemm_tn_slices(N, K), nk = (int64_t)N * K;
+  float* scratch = part + zmax * (nk + N);   // (second-pass buffers, zs > RED_CHUNK only)
+  if (int32_t st = reduce_rows_add(part, zs, nk, dW, scratch, s)) return st;
+  return db ? reduce_rows_add(part_b, zs, N, db, scratch + reduce_scratch_floats(zmax, nk), s) : NRMS_OK;
 }
 
 int32_t launch_transpose(const float* const* src, int nseg, int seg_rows, int cols, float* dst,

@@ -51,13 +51,14 @@ def model_params(model):
 
 class _Scratch:
     def __init__(self):
-        self.buf = None
+        self.bufs = {}
 
-    def get(self, nbytes, dev):
+    def get(self, nbytes, dev, slot="main"):
         nbytes = max(int(nbytes), 256)
-        if self.buf is None or self.buf.numel() < nbytes or self.buf.device != dev:
-            self.buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        return self.buf
+        buf = self.bufs.get(slot)
+        if buf is None or buf.numel() < nbytes or buf.device != dev:
+            buf = self.bufs[slot] = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        return buf
 
 
 _scratch = _Scratch()
@@ -175,7 +176,9 @@ class NRMSTrain(torch.autograd.Function):
                ws.numel(), st)
         dX = torch.empty_like(dXd)
         N.call("nrms_dropout", P(dXd), P(dX), R * D, ctypes.c_float(p), ctypes.c_uint64(s1), st)
-        N.call("nrms_embedding_backward", P(ids), R, P(dX), V, D, 0, P(gE), st)
+        # deterministic (tokens sorted by id, rows summed in token order)
+        ws_e = _scratch.get(lib.nrms_embedding_backward_workspace_size(R, V), dev, slot="embed")
+        N.call("nrms_embedding_backward_ws", P(ids), R, P(dX), V, D, 0, P(gE), P(ws_e), ws_e.numel(), st)
 
         def split(gw, gb):
             return [gw[0:D], gb[0:D], gw[D:2 * D], gb[D:2 * D], gw[2 * D:], gb[2 * D:]]

@@ -191,10 +191,10 @@ def test_rccl_world1_collectives(tmp_path):
     assert r["synced"] == g["synced"] == [False, True]
     for o in (r, g):   # the average over one client is the client's model, bitwise
         assert np.array_equal(o["post"], o["pre"])
-    # same kernels and batches in two processes: equal up to the order of the
-    # training kernels' float atomics, which Adam (lr 1e-4, 2 steps) can turn
-    # into at most a few lr-sized steps on near-zero-gradient entries
-    assert np.abs(r["post"] - g["post"]).max() <= 1e-3
+    # same kernels and batches in two processes: the training kernels are
+    # deterministic (no float atomics), so the trained and
+    # synced parameters agree bitwise across the two backends
+    assert np.array_equal(r["post"], g["post"])
 
 
 def _shard_logits(rank, world, B):

@@ -126,6 +126,53 @@ def test_hip_train_grads_match_aten_with_dropout_masks(device):
     _compare(gh, ga)
 
 
+@pytest.mark.parametrize("gemm", ["f16x3", "f32"])
+def test_hip_train_step_bitwise_deterministic(device, gemm):
+    """The training kernels have no float atomics (split-K partials summed in
+    slice order, per-sequence dq / db partials, the embedding gradient summed
+    per id in token order after a stable sort): three runs of the same step,
+    with dropout, give bitwise the same gradients of every parameter, and the
+    embedding gradient equals the atomic form's within rounding."""
+    from newsrecommendationsystem_amd import _native as N
+    from newsrecommendationsystem_amd import train_hip as H
+    V, B = 900, 8
+    sd = W.nrms_state(41, V)
+    m = _model(sd, V, device, p=0.2)
+    cand, clk = _batch(41, B, V, device=device)
+    mode = {"f16x3": N.NRMS_GEMM_SPLIT_F16X3, "f32": N.NRMS_GEMM_F32}[gemm]
+    runs = []
+    with N.gemm_arith(mode):
+        for _ in range(3):
+            yh = H.forward_hip(m, cand, clk, seed=9)
+            runs.append(_grads(m, yh))
+    for loss, g in runs[1:]:
+        assert loss == runs[0][0]
+        for k in g:
+            assert torch.equal(g[k], runs[0][1][k]), k
+    # the deterministic embedding gradient against the atomic entry point
+    R, D = 4096, 300
+    gen = torch.Generator(device=device).manual_seed(3)
+    ids = torch.randint(0, 64, (R,), generator=gen, device=device)   # many repeats per id
+    ids[::7] = 0                                                      # padding rows skipped
+    dx = torch.randn(R, D, generator=gen, device=device)
+    ga, gd = torch.zeros(V, D, device=device), torch.zeros(V, D, device=device)
+    st = N.stream_handle(device)
+    N.call("nrms_embedding_backward", N.ptr(ids), R, N.ptr(dx), V, D, 0, N.ptr(ga), st)
+    lib = N.load()
+    ws = torch.empty(lib.nrms_embedding_backward_workspace_size(R, V), dtype=torch.uint8, device=device)
+    N.call("nrms_embedding_backward_ws", N.ptr(ids), R, N.ptr(dx), V, D, 0, N.ptr(gd), N.ptr(ws), ws.numel(), st)
+    ref = torch.zeros(V, D, dtype=torch.float64, device=device)
+    keep = ids != 0
+    ref.index_add_(0, ids[keep], dx[keep].double())
+    assert float(gd[0].abs().max()) == 0.0 and float(gd[64:].abs().max()) == 0.0
+    assert float((gd.double() - ref).abs().max()) <= 1e-5 * float(ref.abs().max())
+    assert float((gd - ga).abs().max()) <= 1e-5 * float(ref.abs().max())
+    # in token order: the CPU reference's index_add on the same rows, bitwise
+    cpu = torch.zeros(V, D)
+    cpu.index_add_(0, ids[keep].cpu(), dx[keep].cpu())
+    assert torch.equal(gd.cpu(), cpu)
+
+
 @pytest.mark.parametrize("per_param", [False, True])
 @pytest.mark.parametrize("n_tensors", [4, 41])   # 41 > 32: two kernarg chunks
 def test_hip_adam_matches_torch_adam(device, monkeypatch, per_param, n_tensors):
