@@ -177,6 +177,10 @@ int32_t nrms_behaviors_parse(const char* buf, int64_t len, const int64_t* capaci
   if ((cap_lines && (!fields || !cand_count || !hist_count || !hist_user)) || (cap_cand && (!cand_num || !labels)) ||
       (cap_hist && !hist_num))
     return NRMS_ERR_INVALID_ARG;
+  // the same byte check as nrms_behaviors_scan ('\r', '\v', '\f', non-ASCII:
+  // outside the plain MIND form -> the Python readers), so a caller that skips
+  // the scan cannot get such columns accepted
+  if (!plain_bytes(buf, len)) return NRMS_ERR_UNSUPPORTED;
   // the user key is the history string as data.read_behaviors keeps it (an
   // empty field becomes " "), users numbered in first-seen order (EvalPlan)
   std::unordered_map<std::string_view, int64_t> users;

@@ -708,7 +708,6 @@ static std::atomic<int> g_user_lpt{[] {
   const char* e = getenv("NRMS_USER_LPT");
   return (e && e[0] == '0') ? 0 : 1;
 }()};
-int set_user_lpt(int on) { return g_user_lpt.exchange(on ? 1 : 0); }
 bool user_lpt() { return g_user_lpt.load(std::memory_order_relaxed) != 0; }
 
 bool fused_user_supported(int L, int D, int H, int Q) {

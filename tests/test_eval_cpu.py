@@ -275,3 +275,25 @@ def test_native_behaviors_edge_forms(tmp_path):
                 "id\ttitle\nN1\t(1, 2)\n", "idx\ttitle\nN1\t[1, 2]\n", "id\ttitle\r\nN1\t[1, 2]\r\n"):
         _write(n, bad)
         assert Dt.read_news_parsed_native(n, num_words_title=2) is None, repr(bad)
+
+
+def test_behaviors_parse_checks_bytes_without_scan():
+    """nrms_behaviors_parse called without a preceding nrms_behaviors_scan
+    rejects a non-plain buffer itself (non-ASCII user column, CR line end):
+    NRMS_ERR_UNSUPPORTED, as the header promises (round-4 advisor finding)."""
+    from newsrecommendationsystem_amd import _native as N
+    lib = N.load()
+    P = lambda a: a.ctypes.data
+    for text in ("1\tU\xe9\tt\tN1\tN3-1\n", "1\tU1\tt\tN1\tN3-1\r\n", "1\tU1\tt\tN1\tN3-1\n"):
+        buf = text.encode("utf-8")
+        cap = np.array([4, 8, 8], np.int64)
+        fields = np.zeros((4, 5, 2), np.int64)
+        cand_num, labels, cand_count = np.zeros(8, np.int64), np.zeros(8, np.int32), np.zeros(4, np.int64)
+        hist_num, hist_count, hist_user = np.zeros(8, np.int64), np.zeros(4, np.int64), np.zeros(4, np.int64)
+        counts = np.zeros(4, np.int64)
+        st = lib.nrms_behaviors_parse(buf, len(buf), P(cap), P(counts), P(fields), P(cand_num), P(labels),
+                                      P(cand_count), P(hist_num), P(hist_count), P(hist_user))
+        if text.endswith("N3-1\n") and "\xe9" not in text:
+            assert st == N.NRMS_OK and counts[0] == 1 and cand_num[0] == 3 and labels[0] == 1
+        else:
+            assert st == N.NRMS_ERR_UNSUPPORTED, repr(text)

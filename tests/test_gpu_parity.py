@@ -1088,3 +1088,44 @@ def test_forward_timed_matches_forward_and_records_stages(device):
     lib = N.load()
     assert lib.nrms_forward_timed(None, None, B, 5, 50, 20, None, V, None, None, 2, None, None, 0,
                                   None, None, 3) == N.NRMS_ERR_INVALID_ARG
+
+
+_FALLBACK_SCRIPT = r"""
+import sys, torch, numpy as np
+sys.path.insert(0, sys.argv[1])
+from oracle import weights as W
+from newsrecommendationsystem_amd import NRMS, NRMSConfig
+from newsrecommendationsystem_amd.pipeline import ForwardPlan
+V, B = 3000, 300
+class Cfg(NRMSConfig):
+    num_words = V
+m = NRMS(Cfg)
+m.load_state_dict({k: torch.from_numpy(v) for k, v in W.nrms_state(9, V).items()})
+m = m.to("cuda:0").eval()
+cand, clk, _ = W.impressions(9, 78, B, V)
+clk = clk.copy()
+clk[np.random.default_rng(9).random(clk.shape[:2]) < 0.25] = 0
+c, k = torch.from_numpy(cand).cuda(), torch.from_numpy(clk).cuda()
+with torch.no_grad():
+    y = ForwardPlan(m, B, 5, 50, 20, proj_mode=2, fused=True).run(c, k).clone()
+    ref = m.forward_ids(c, k, proj_mode=2)
+assert torch.isfinite(ref).all()
+assert torch.equal(y, ref), float((y - ref).abs().max())
+print("FALLBACK_OK")
+"""
+
+
+def test_forward_classification_fallback_without_tail_jobs():
+    """nrms_forward with the classification's first half run in the pack
+    launch but the projection's tail jobs skipped (NRMS_TEST_SKIP_CLASSIFY_TAIL,
+    read at library load: a child process): the news launch classifies again
+    with its own atomics, on counters the pack launch reset, and the logits
+    equal the stage-by-stage plan's bitwise (round-4 advisor finding)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, NRMS_TEST_SKIP_CLASSIFY_TAIL="1")
+    r = subprocess.run([sys.executable, "-c", _FALLBACK_SCRIPT, root], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "FALLBACK_OK" in r.stdout, r.stderr[-3000:]
