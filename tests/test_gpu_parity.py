@@ -466,12 +466,14 @@ def test_qkv_project_ws_vs_staged_gemm(device, gemm_mode, case):
     assert (got[:, 900:] == 7.0).all()   # the row padding is not written
 
 
-def test_qkv_project_f16x3_range(device):
+@pytest.mark.parametrize("M", [300, 20001])
+def test_qkv_project_f16x3_range(device, M):
     """The f16x3 projection's power-of-two scaling (proj_x6.hip): A rows from
     1e-20 to 1e30 in magnitude (beyond fp16's range both ways) against W_Q
     scaled by 1e5 and W_K by 1e-8 project within 2e-6 of the fp64 oracle per
     row and per Q / K / V segment; an all-zero row gives exactly the bias, a
-    row holding an inf gives NaN."""
+    row holding an inf gives NaN; at M = 300 and at M = 20,001 (313 row
+    tiles, a partial last one)."""
     from newsrecommendationsystem_amd import _native as N
     sd = dict(W.nrms_state(5, 64))
     p = "news_encoder.multihead_self_attention"
@@ -480,10 +482,10 @@ def test_qkv_project_f16x3_range(device):
     m = _module(sd, 64, device)
     w, keep = m.news_encoder.weights()
     rng = np.random.default_rng(3)
-    M = 300
     xs = rng.standard_normal((M, 300)) * 10.0 ** rng.uniform(-20, 30, (M, 1))
-    xs[7] = 0.0
-    xs[11, 5] = np.inf
+    zero_rows, inf_rows = [7, M - 1], [11, M - 2]
+    xs[zero_rows] = 0.0
+    xs[inf_rows, 5] = np.inf
     X = torch.from_numpy(xs.astype(np.float32)).to(device)
     got = torch.empty(M, 900, device=device)
     nb = N.load().nrms_qkv_project_workspace_size(300)
@@ -495,12 +497,13 @@ def test_qkv_project_f16x3_range(device):
     g = _np(got)
     xa = X.cpu().numpy().astype(np.float64)
     fine = np.ones(M, bool)
-    fine[[7, 11]] = False
+    fine[zero_rows + inf_rows] = False
     for i, n_ in enumerate(("W_Q", "W_K", "W_V")):
         want = O.linear(xa[fine], sd[f"{p}.{n_}.weight"], sd[f"{p}.{n_}.bias"], np.float64)
         assert O.normwise_rel_err(g[fine, 300 * i:300 * (i + 1)], want).max() < 2e-6, n_
-        assert np.array_equal(g[7, 300 * i:300 * (i + 1)], sd[f"{p}.{n_}.bias"])
-    assert np.isnan(g[11]).all()
+        for z in zero_rows:
+            assert np.array_equal(g[z, 300 * i:300 * (i + 1)], sd[f"{p}.{n_}.bias"])
+    assert np.isnan(g[inf_rows]).all()
 
 
 @pytest.mark.parametrize("fused", [True, False])
@@ -1129,3 +1132,4 @@ def test_forward_classification_fallback_without_tail_jobs():
     r = subprocess.run([sys.executable, "-c", _FALLBACK_SCRIPT, root], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "FALLBACK_OK" in r.stdout, r.stderr[-3000:]
+
