@@ -864,7 +864,9 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           // query column i's Q slices are dead: the next group's go into them
           // (main pass: the next group is of this bucket or a smaller one, so
           // its queries are tokens < 4 NB; slots past its rows read the zero row)
+#ifndef NRMS_PROBE_NO_QLOAD   // (probe builds: the phase without its gather loads)
           if constexpr (!EXACT) prefetch_q_tok(nbuf, i);
+#endif
           s_exp(i);
           o_mfma(i);
           o_store(i);
@@ -1078,7 +1080,11 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         // row), no zero fill. The recheck pass walks groups of any bucket.
 #pragma unroll
         for (int mt = 0; mt < NB; ++mt) {
+#ifndef NRMS_PROBE_NO_KLOAD
           if constexpr (!EXACT) prefetch_k_tok(nbuf, mt);
+#else
+          if constexpr (!EXACT) {}
+#endif
           else if (mt < nb_next) prefetch_qk_tok(nbuf, mt);
           else zero_qk_tok(mt);
           __builtin_amdgcn_sched_barrier(0);
@@ -1210,8 +1216,10 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         if constexpr (EXACT) {
           prefetch_v(nbuf, nb_next);
         } else {
+#ifndef NRMS_PROBE_NO_VLOAD
 #pragma unroll
           for (int kk = 0; kk < LR; ++kk) prefetch_v_tok(nbuf, kk);   // (as the Q|K slices above)
+#endif
         }
       }
       NRMS_STAMP(6)
