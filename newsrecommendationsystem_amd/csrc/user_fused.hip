@@ -132,12 +132,14 @@ __global__ __launch_bounds__(UORD_T) void user_order_kernel(const uint8_t* __res
   if (u < B) order[(int64_t)blockIdx.x * UORD_T + atomicAdd(&base[le], 1)] = (int32_t)u;
 }
 
-template <int MODE, int LMAX, int NT>
+template <int MODE, int LMAX, int NT, int KVR = LMAX>
 __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     const float* __restrict__ qkv, int64_t ldq, int L_all, const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
     PaddingGroups pg, int uflags, const int32_t* __restrict__ order, ScoreFold sf) {
-  static_assert(NT >= UH * LMAX, "one (head, query) task per thread");
+  constexpr bool CHUNKED = KVR < LMAX;   // (see the attention below)
+  static_assert(CHUNKED || NT >= UH * LMAX, "one (head, query) task per thread");
+  static_assert(!CHUNKED || MODE == 2, "the chunked instance is split-f16 only");
   constexpr int NW = NT / 64;
   constexpr int NTPW = (UNT + NW - 1) / NW;            // N-tiles per wave
   constexpr int MT = (LMAX + 15) / 16;                 // M-tiles
@@ -153,8 +155,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 #else
 #define NRMS_U_STAMP(k)
 #endif
-  float* tile = ulds;                                  // [LMAX][URS]
-  float* part = tile + LMAX * URS;                     // [UNT][64]
+  float* tile = ulds;                                  // [KVR][URS]
+  float* part = tile + KVR * URS;                      // [UNT][64]
   float* wts = part + UNT * 64;                        // [64]
   // MODE 2: part | wts | [64] hold one max |ctx| per (head, query) thread
   // until the split; then [64] row exponents ea
@@ -197,51 +199,59 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   };
 
   // ---------------- 0. stage K|V (all loads in flight at once), q slices ----------------
-  const bool has = tid < UH * L;
-  const int h = has ? tid / L : 0, qi = has ? tid - h * L : 0;
-  float q[UDK];
-  {
-    const float4* qp = reinterpret_cast<const float4*>(row(qi) + UDK * h);
-#pragma unroll
-    for (int t = 0; t < UDK / 4; ++t) {
-      const float4 v = qp[t];
-      q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
+  // LDS-DMA (global_load_lds_dwordx4): the tile's rows are the K|V rows back
+  // to back (2,400 B each), so wave-instruction p fills bytes 1,024 p .. +
+  // 1,023 of it, each lane from its own row; lanes past the last row reload
+  // its last 16 B into the LDS after the staged rows (unused rows, or part:
+  // free until the attention's end). (Register staging: user_fused 2.1 us
+  // slower, profiles/r4m_user_staging_gemm_ab.txt)
+  auto stage = [&](int r0, int nr) __attribute__((always_inline)) {
+    const int nbytes = nr * URS * 4;
+    const int npieces = (nbytes + 1023) >> 10;
+    for (int p = w; p < npieces; p += NT / 64) {
+      int o = (p << 10) + 16 * lane;
+      o = o < nbytes ? o : nbytes - 16;
+      const int i = o / (URS * 4), wb = o - i * (URS * 4);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(row(r0 + i) + UD + (wb >> 2)),
+                                       (__attribute__((address_space(3))) void*)(tile + (p << 8)), 16, 0, 0);
     }
-    // LDS-DMA (global_load_lds_dwordx4): the tile's rows are the K|V rows
-    // back to back (2,400 B each), so wave-instruction p fills bytes
-    // 1,024 p .. + 1,023 of it, each lane from its own row; lanes past the
-    // last row reload its last 16 B into the LDS after the L rows (unused
-    // rows, or part: free until the attention's end). (Register staging:
-    // user_fused 2.1 us slower, profiles/r4m_user_staging_gemm_ab.txt)
+  };
+  // CHUNKED (the 512-thread, 80-KB instance for histories of 33..50 titles,
+  // two workgroups per CU): the K|V rows are staged KVR at a time (the keys in
+  // order, each chunk behind a barrier), and a user with more (head, query)
+  // tasks than threads runs them in two passes (the first pass's context kept
+  // in registers): the same per-task arithmetic in the same key order as the
+  // whole-tile instances.
+  const int ntask = UH * L;
+  const int npass = CHUNKED ? (ntask + NT - 1) / NT : 1;    // (workgroup-uniform)
+  const int nchunk = CHUNKED ? (L + KVR - 1) / KVR : 1;
+  static_assert(!CHUNKED || UH * LMAX <= 2 * NT, "at most two task passes");
+  static_assert(MODE != 2 || UNT * 64 + 64 + 64 >= UH * LMAX, "per-thread max slots before rexp");
+  // exp(d / sqrt(d_k)) as v_exp_f32(d · log2(e) / sqrt(d_k)), as the news kernel
+  const float rs = 1.4426950408889634f / sqrtf((float)UDK);
+  const float sqrt_dk = sqrtf((float)UDK);
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  float acc[UDK], q[UDK];
+  [[maybe_unused]] float acc0[UDK];   // CHUNKED, two passes: the first pass's context
+  float mrow = 0.f, mrow0 = 0.f;      // MODE 2: max |ctx| of this thread's task (per pass)
+  for (int pass = 0; pass < npass; ++pass) {
+    const int task = tid + pass * NT;
+    const bool has = task < ntask;
+    const int h = has ? task / L : 0, qi = has ? task - h * L : 0;
     {
-      const int nbytes = L * URS * 4;
-      const int npieces = (nbytes + 1023) >> 10;
-      for (int p = w; p < npieces; p += NT / 64) {
-        int o = (p << 10) + 16 * lane;
-        o = o < nbytes ? o : nbytes - 16;
-        const int i = o / (URS * 4), wb = o - i * (URS * 4);
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(row(i) + UD + (wb >> 2)),
-                                         (__attribute__((address_space(3))) void*)(tile + (p << 8)), 16, 0, 0);
+      const float4* qp = reinterpret_cast<const float4*>(row(qi) + UDK * h);
+#pragma unroll
+      for (int t = 0; t < UDK / 4; ++t) {
+        const float4 v = qp[t];
+        q[4 * t] = v.x; q[4 * t + 1] = v.y; q[4 * t + 2] = v.z; q[4 * t + 3] = v.w;
       }
     }
-  }
-  static_assert(MODE != 2 || UNT * 64 + 64 + 64 >= UH * LMAX, "per-thread max slots before rexp");
-  __syncthreads();
-  NRMS_U_STAMP(0)   // K|V staged
-
-  // ---------------- 1. attention: thread = (head, query) ----------------
-  float acc[UDK];
-  if (has) {
-    // exp(d / sqrt(d_k)) as v_exp_f32(d · log2(e) / sqrt(d_k)), as the news kernel
-    const float rs = 1.4426950408889634f / sqrtf((float)UDK);
-    const float sqrt_dk = sqrtf((float)UDK);
     // packed FP32 (v_pk_fma_f32, two FMAs per lane per instruction): the dot
     // product as even / odd partial sums added at the end, the context update
     // elementwise (the same FMAs as the scalar form): user_fused -1.3 us
-    // (profiles/r4o_user_pk_fma_ab.txt)
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    auto dot = [&](int j) __attribute__((always_inline)) {
-      const float4* kr = reinterpret_cast<const float4*>(tile + j * URS + UDK * h);
+    // (profiles/r4o_user_pk_fma_ab.txt). kv: the K|V row (K at kv, V at kv + UD).
+    auto dot = [&](const float* kv) __attribute__((always_inline)) {
+      const float4* kr = reinterpret_cast<const float4*>(kv + UDK * h);
       f2 d = f2{0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
@@ -251,8 +261,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       }
       return d.x + d.y;
     };
-    auto axpy = [&](float a, int j) __attribute__((always_inline)) {
-      const float4* vr = reinterpret_cast<const float4*>(tile + j * URS + UD + UDK * h);
+    auto axpy = [&](float a, const float* kv) __attribute__((always_inline)) {
+      const float4* vr = reinterpret_cast<const float4*>(kv + UD + UDK * h);
       const f2 a2 = f2{a, a};
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
@@ -265,99 +275,152 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 #pragma unroll
     for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
     // Fast path, one pass over the user's L keys (a rolled loop, four keys per
-    // iteration: their dot products interleave; keys past L in the last
-    // iteration read row L-1 with weight 0): sum = the raw exps in the
-    // reference's key order (row 0 counted m0 times, one addition at a time),
-    // acc = sum_j e_j v_j, ctx = acc / (sum + 1e-8). Only the normalisation
-    // moves (after the sum instead of per weight: fp32 rounding). No exp is
-    // kept, so the work is ~L, not LMAX, keys per query.
+    // iteration: their dot products interleave; keys past the staged rows in
+    // the last iteration read the last one with weight 0): sum = the raw exps
+    // in the reference's key order (row 0 counted m0 times, one addition at a
+    // time), acc = sum_j e_j v_j, ctx = acc / (sum + 1e-8). Only the
+    // normalisation moves (after the sum instead of per weight: fp32
+    // rounding). No exp is kept, so the work is ~L, not LMAX, keys per query.
     float sum = 0.f;
-    for (int j0 = 0; j0 < L; j0 += 4) {
-      float e[4];
+    for (int c = 0; c < nchunk; ++c) {
+      const int kb = c * KVR, ke = CHUNKED ? (L < kb + KVR ? L : kb + KVR) : L;
+      if (CHUNKED && (pass > 0 || c > 0)) __syncthreads();   // the previous chunk's readers are done
+      stage(kb, ke - kb);
+      __syncthreads();
+      if (c == 0 && pass == 0) { NRMS_U_STAMP(0) }   // K|V staged
+      if (has) {
+        const float* kt = tile - (int64_t)kb * URS;   // key j's K|V row: kt + j URS
+        for (int j0 = kb; j0 < ke; j0 += 4) {
+          float e[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int j = j0 + u;
-        e[u] = j < L ? __builtin_amdgcn_exp2f(dot(j < L ? j : L - 1) * rs) : 0.f;
+          for (int u = 0; u < 4; ++u) {
+            const int j = j0 + u;
+            e[u] = j < ke ? __builtin_amdgcn_exp2f(dot(kt + (j < ke ? j : ke - 1) * URS) * rs) : 0.f;
+          }
+          if (j0 == 0) {
+            for (int cc = 0; cc < m0; ++cc) sum += e[0];   // (row 0's multiplicity)
+            e[0] *= (float)m0;
+          } else {
+            sum += e[0];
+          }
+          sum += e[1];
+          sum += e[2];
+          sum += e[3];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) axpy(e[u], kt + (j0 + u < ke ? j0 + u : ke - 1) * URS);
+        }
       }
-      if (j0 == 0) {
-        for (int c = 0; c < m0; ++c) sum += e[0];   // (row 0's multiplicity)
-        e[0] *= (float)m0;
+    }
+    if (has) {
+      bool finite = true;
+#pragma unroll
+      for (int t = 0; t < UDK; ++t) finite &= __builtin_isfinite(acc[t]);
+      if (!exp_row_needs_recheck(sum) && finite) {
+        const float inv = 1.0f / (sum + 1e-8f);
+#pragma unroll
+        for (int t = 0; t < UDK; ++t) acc[t] *= inv;
       } else {
-        sum += e[0];
+        // rare (rows near fp32 overflow, non-finite inputs, or a context past
+        // fp32 before the normalisation): the reference's own arithmetic and
+        // order -- ref_exp weights, e_j / (sum + 1e-8) per key, then sum_j P_j v_j
+        // (kExpRecheck); the exps are recomputed in the second pass. The K|V
+        // rows from the tile, or (CHUNKED: only the last chunk is staged) from
+        // the projected rows themselves.
+        auto kvr = [&](int j) -> const float* { return CHUNKED ? row(j) + UD : tile + j * URS; };
+        sum = 0.f;
+        for (int j = 0; j < L; ++j) {
+          const float x = ref_exp(dot(kvr(j)), sqrt_dk);
+          if (j == 0)
+            for (int cc = 0; cc < m0; ++cc) sum += x;
+          else
+            sum += x;
+        }
+        const float inv = 1.0f / (sum + 1e-8f);
+#pragma unroll
+        for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
+        for (int j = 0; j < L; ++j) {
+          float a = ref_exp(dot(kvr(j)), sqrt_dk) * inv;
+          if (j == 0 && m0 > 1) a *= (float)m0;
+          axpy(a, kvr(j));
+        }
       }
-      sum += e[1];
-      sum += e[2];
-      sum += e[3];
+      if constexpr (MODE == 2) {
+        float m = 0.f;
 #pragma unroll
-      for (int u = 0; u < 4; ++u) axpy(e[u], j0 + u < L ? j0 + u : L - 1);
-    }
-    bool finite = true;
-#pragma unroll
-    for (int t = 0; t < UDK; ++t) finite &= __builtin_isfinite(acc[t]);
-    if (!exp_row_needs_recheck(sum) && finite) {
-      const float inv = 1.0f / (sum + 1e-8f);
-#pragma unroll
-      for (int t = 0; t < UDK; ++t) acc[t] *= inv;
-    } else {
-      // rare (rows near fp32 overflow, non-finite inputs, or a context past
-      // fp32 before the normalisation): the reference's own arithmetic and
-      // order -- ref_exp weights, e_j / (sum + 1e-8) per key, then sum_j P_j v_j
-      // (kExpRecheck); the exps are recomputed in the second pass
-      sum = 0.f;
-      for (int j = 0; j < L; ++j) {
-        const float x = ref_exp(dot(j), sqrt_dk);
-        if (j == 0)
-          for (int c = 0; c < m0; ++c) sum += x;
-        else
-          sum += x;
-      }
-      const float inv = 1.0f / (sum + 1e-8f);
-#pragma unroll
-      for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
-      for (int j = 0; j < L; ++j) {
-        float a = ref_exp(dot(j), sqrt_dk) * inv;
-        if (j == 0 && m0 > 1) a *= (float)m0;
-        axpy(a, j);
+        for (int t = 0; t < UDK; ++t) m = fmaxf(m, fabsf(acc[t]));
+        mrow = m;
+        // (one slot per (head, query) task in part | wts | rmax; the row max
+        // after the barrier; CHUNKED: written after the last chunk's readers,
+        // as a later chunk's staging may run past the tile into part)
+        if constexpr (!CHUNKED) part[task] = m;
       }
     }
-    if constexpr (MODE == 2) {
-      float m = 0.f;
+    if constexpr (CHUNKED) {
+      if (pass == 0 && npass > 1) {
 #pragma unroll
-      for (int t = 0; t < UDK; ++t) m = fmaxf(m, fabsf(acc[t]));
-      part[tid] = m;   // (one slot per (head, query) thread in part | wts | rmax; the row max after the barrier)
+        for (int t = 0; t < UDK; ++t) acc0[t] = acc[t];
+        mrow0 = mrow;
+      }
     }
   }
   __syncthreads();   // every K|V read done: the tile becomes the context
   NRMS_U_STAMP(1)   // attention
+  // the context's row stride in halves (and its planes): the whole-tile
+  // instances keep each row at its K|V row (2,400 B, three planes);
+  // CHUNKED packs them (1,952 B, three planes; past 39 rows 1,312 B and two
+  // planes, hi | lo: the pooling then rebuilds the context from those two,
+  // 22 bits, as the GEMM reads it). Both strides conflict-free for the GEMM's
+  // fragment reads.
+  const bool three = !CHUNKED || L * 1952 <= KVR * URS * 4;
+  const int cs = !CHUNKED ? 2 * URS : (three ? 976 : 656);
+  const int npl = three ? 3 : 2;
+  const int h = tid < ntask ? tid / L : 0, qi = tid < ntask ? tid - h * L : 0;   // (the first pass's task)
+  const bool has = tid < ntask;
   if constexpr (MODE == 2) {
+    if constexpr (CHUNKED) {
+      if (has) part[tid] = npass > 1 ? mrow0 : mrow;
+      if (npass > 1 && tid + NT < ntask) part[tid + NT] = mrow;
+      __syncthreads();
+    }
     // three fp16 planes per row (hi | lo | r), in the MODE 1 positions
     _Float16* t16 = reinterpret_cast<_Float16*>(tile);
-    if (has) {
+    auto write_ctx = [&](int task, const float (&a)[UDK]) __attribute__((always_inline)) {
+      const int th = task / L, tq = task - th * L;
       float mx = 0.f;
-      for (int hh = 0; hh < UH; ++hh) mx = fmaxf(mx, part[hh * L + qi]);   // the row's 15 head threads
+      for (int hh = 0; hh < UH; ++hh) mx = fmaxf(mx, part[hh * L + tq]);   // the row's 15 head tasks
       const int ea = pk::exp_field(mx) - 3;
-      if (h == 0) rexp[qi] = ea;
+      if (th == 0) rexp[tq] = ea;
 #pragma unroll
       for (int g = 0; g < UDK / 4; ++g) {
         _Float16 hv[3][4];
 #pragma unroll
         for (int x = 0; x < 4; ++x) {
-          const float v = ldexpf(acc[4 * g + x], -ea);
+          const float v = ldexpf(a[4 * g + x], -ea);
           hv[0][x] = (_Float16)v;
           const float r1 = (v - (float)hv[0][x]) * kF16LoScale;   // exact
           hv[1][x] = (_Float16)r1;
           hv[2][x] = (_Float16)(r1 - (float)hv[1][x]);
         }
-        const int pos = qi * (2 * URS) + ukpos(UDK * h + 4 * g);
+        const int pos = tq * cs + ukpos(UDK * th + 4 * g);
 #pragma unroll
         for (int pl = 0; pl < 3; ++pl)
-          *reinterpret_cast<uf16x4*>(t16 + pos + UKP * pl) = uf16x4{hv[pl][0], hv[pl][1], hv[pl][2], hv[pl][3]};
+          if (pl < npl) *reinterpret_cast<uf16x4*>(t16 + pos + UKP * pl) = uf16x4{hv[pl][0], hv[pl][1], hv[pl][2], hv[pl][3]};
       }
+    };
+    if constexpr (CHUNKED) {
+      if (npass > 1) {
+        if (has) write_ctx(tid, acc0);
+        if (tid + NT < ntask) write_ctx(tid + NT, acc);
+      } else if (has) {
+        write_ctx(tid, acc);
+      }
+    } else if (has) {
+      write_ctx(tid, acc);
     }
     uint16_t* z16 = reinterpret_cast<uint16_t*>(tile);
     for (int e = tid; e < L * 15; e += NT) {   // K padding 300..319, each plane
       const int i = e / 15, g = (e % 15) % 5, pl = (e % 15) / 5;
-      *reinterpret_cast<uint2*>(z16 + i * (2 * URS) + UKP * pl + ukpos(UD + 4 * g)) = make_uint2(0u, 0u);
+      if (pl < npl) *reinterpret_cast<uint2*>(z16 + i * cs + UKP * pl + ukpos(UD + 4 * g)) = make_uint2(0u, 0u);
     }
   } else if constexpr (MODE == 1) {
     // three bf16 planes per row (plane p at bf16 offset 320 p), k permuted to
@@ -411,11 +474,12 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       bv[j] = ok ? b_add[col] : 0.f;
       if constexpr (MODE == 2) ewv[j] = nt < UNT ? reinterpret_cast<const int32_t*>(WaP)[pk::USER_H3_EXP + col] : 0;
     }
-    int arow[MT];
+    int arow[MT], arow16[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const int r = 16 * mt + lm;
       arow[mt] = (r < L ? r : L - 1) * URS;
+      arow16[mt] = (r < L ? r : L - 1) * cs;   // (MODE 2: the context's stride in halves)
     }
     floatx4 c[MT][NTPW];
 #pragma unroll
@@ -446,7 +510,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int pl = 0; pl < 2; ++pl)
-            a[mt][pl] = *reinterpret_cast<const uf16x8*>(t16 + 2 * arow[mt] + UKP * pl + 32 * ks + 8 * kq);
+            a[mt][pl] = *reinterpret_cast<const uf16x8*>(t16 + arow16[mt] + UKP * pl + 32 * ks + 8 * kq);
 #pragma unroll
         for (int j = 0; j < NTPW; ++j) {
           const int nt = w + NW * j;
@@ -605,10 +669,10 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         const float wi = wts[i];
         float4 cv;
         if constexpr (MODE == 2) {   // ldexp(hi + 2^-11 (lo + r), ea): the fp32 context (see MODE 2)
-          const _Float16* t16 = reinterpret_cast<const _Float16*>(tile) + i * (2 * URS) + ukpos(4 * u);
+          const _Float16* t16 = reinterpret_cast<const _Float16*>(tile) + i * cs + ukpos(4 * u);
           const uf16x4 p0 = *reinterpret_cast<const uf16x4*>(t16);
           const uf16x4 p1 = *reinterpret_cast<const uf16x4*>(t16 + UKP);
-          const uf16x4 p2 = *reinterpret_cast<const uf16x4*>(t16 + 2 * UKP);
+          const uf16x4 p2 = three ? *reinterpret_cast<const uf16x4*>(t16 + 2 * UKP) : uf16x4{0, 0, 0, 0};
           const int ea = rexp[i];
           cv.x = ldexpf((float)p0[0] + ((float)p1[0] + (float)p2[0]) * kF16LoUnscale, ea);
           cv.y = ldexpf((float)p0[1] + ((float)p1[1] + (float)p2[1]) * kF16LoUnscale, ea);
@@ -679,24 +743,42 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 #endif
 }
 
-template <int MODE, int LMAX, int NT>
+template <int MODE, int LMAX, int NT, int KVR = LMAX>
 int32_t launch_user_inst(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
                          PaddingGroups pg, int uflags, const int32_t* order, const ScoreFold& sf) {
-  const size_t lds = ((size_t)LMAX * URS + UNT * 64 + 64 + 2 * 64) * 4;
-  ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT>), (int)lds);
-  hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
+  const size_t lds = ((size_t)KVR * URS + UNT * 64 + 64 + 2 * 64) * 4;
+  ensure_dynamic_lds(reinterpret_cast<const void*>(&fused_user_kernel<MODE, LMAX, NT, KVR>), (int)lds);
+  hipLaunchKernelGGL((fused_user_kernel<MODE, LMAX, NT, KVR>), dim3((unsigned)B), dim3(NT), lds, s, qkv,
                      ldq, L, wap, b_add, q_add, out, pg, uflags, order, sf);
   return launch_status();
 }
+
+static std::atomic<int> g_user_chunk{[] {
+  const char* e = getenv("NRMS_USER_CHUNK");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
+
+// (measurement only) NRMS_USER_LMAX=n: take the instance of the smallest LMAX >= max(L, n)
+static const int g_user_lmax_min = [] {
+  const char* e = getenv("NRMS_USER_LMAX");
+  return e ? atoi(e) : 0;
+}();
 
 template <int MODE>
 int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const float* wap,
                          const float* b_add, const float* q_add, float* out, hipStream_t s,
                          PaddingGroups pg, int uflags, const int32_t* order, const ScoreFold& sf) {
-  if (L <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
-  if (L <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
-  if (L <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
+  const int Li = L > g_user_lmax_min ? L : g_user_lmax_min;
+  // 33..50-title histories, split-f16: 512 threads and 80 KB of LDS (K|V
+  // staged 32 rows at a time), so two workgroups share a CU
+  // (NRMS_USER_CHUNK=0: the 832-thread whole-tile instance)
+  if constexpr (MODE == 2)
+    if (Li > 32 && Li <= 50 && g_user_chunk.load(std::memory_order_relaxed))
+      return launch_user_inst<MODE, 50, 512, 32>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
+  if (Li <= 16) return launch_user_inst<MODE, 16, 256>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
+  if (Li <= 32) return launch_user_inst<MODE, 32, 512>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
+  if (Li <= 50) return launch_user_inst<MODE, 50, 832>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
   return launch_user_inst<MODE, 64, 1024>(qkv, ldq, B, L, wap, b_add, q_add, out, s, pg, uflags, order, sf);
 }
 

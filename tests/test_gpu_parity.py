@@ -814,6 +814,48 @@ def test_fused_user_tail_value_range(device, gemm_mode):
     assert err < 1e-5, float(err)
 
 
+@pytest.mark.parametrize("n_clk", [33, 36, 50])
+def test_user_tail_recheck_rows_chunked(device, gemm_mode, n_clk):
+    """Histories of 33-50 titles (split-f16: the 512-thread instance, K|V
+    staged 32 rows at a time, two task passes past 34 titles, the context in
+    two planes past 39): users whose head-0 raw exps come near fp32 overflow
+    (sum >= 2^120, the recheck path, which re-reads K|V from the projected
+    rows) or overflow (NaN, multihead_self.py:16-20) beside ordinary users.
+    Same NaN pattern as the stage kernels, finite users within 1e-5."""
+    from newsrecommendationsystem_amd import _native as N
+    V, B = 300, 24
+    sd = W.nrms_state(37, V)
+    m = _module(sd, V, device)
+    w, keep = m.user_encoder.weights()
+    rng = np.random.default_rng(43 + n_clk)
+    qkv = (0.3 * rng.standard_normal((B, n_clk, 900))).astype(np.float32)
+    for b in range(B):
+        if b % 3:
+            a = 4.36 if b % 3 == 1 else 4.5    # sqrt(20) a^2 = 85.0 (finite, rechecked) / 90.6 (overflow)
+            qkv[b, :, 0:20] = a                 # head 0's Q
+            qkv[b, :, 300:320] = a              # head 0's K
+    x = torch.from_numpy(qkv.reshape(B * n_clk, 900)).to(device)
+    st = N.stream_handle(device)
+    lib = N.load()
+    out = torch.empty(B, 300, device=device)
+    nb = lib.nrms_user_attention_pool_workspace_size(B, n_clk, 300)
+    ws = torch.empty(nb, dtype=torch.uint8, device=device)
+    N.call("nrms_user_attention_pool", N.ptr(x), 0, B, n_clk, ctypes.byref(w), N.ptr(out), N.ptr(ws), nb, st)
+    ctx = torch.empty(B * n_clk, 300, device=device)
+    sc = torch.empty(B * n_clk, device=device)
+    ref = torch.empty(B, 300, device=device)
+    N.call("nrms_self_attention", N.ptr(x), B * n_clk, None, B, None, B, n_clk, ctypes.byref(w), N.ptr(ctx), st)
+    N.call("nrms_additive_attention", N.ptr(ctx), B, n_clk, ctypes.byref(w), N.ptr(sc), N.ptr(ref), st)
+    torch.cuda.synchronize()
+    o, r = _np(out), _np(ref)
+    assert np.array_equal(np.isnan(o), np.isnan(r))
+    nan_users = np.isnan(r).any(axis=1)
+    assert nan_users[2::3].all() and not nan_users[0::3].any() and not nan_users[1::3].any()
+    fin = ~nan_users
+    err = np.linalg.norm(o[fin] - r[fin], axis=1) / np.linalg.norm(r[fin], axis=1)
+    assert err.max() < 1e-5, float(err.max())
+
+
 @pytest.mark.parametrize("n_clk", [65, 200])
 def test_user_tail_beyond_fused_range(device, n_clk):
     """Histories longer than 64: the fused kernel declines (UNSUPPORTED) and
