@@ -1,15 +1,13 @@
 #!/usr/bin/env bash
-# r5f: deterministic training kernels, two-pass column reductions -- train tests + speed vs HEAD
+# r5f: round-5 final build check: full GPU suite, smoke, the driver's bench
+# command, and the profile recipe (trace, traffic, SQ passes)
 set -uo pipefail
 O=gpurun_out/r5f; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_train.py tests/test_gpu_multiprocess.py -m gpu -k "train or rccl_world1_collectives or fedavg_hip" > $O/tests.txt 2>&1 || { tail -40 $O/tests.txt; exit 1; }
-tail -1 $O/tests.txt
-for rep in 1 2 3; do
-  for d in _ab/head .; do
-    (cd $d && timeout -k 10 120 python -m newsrecommendationsystem_amd.train --steps 200 --batch 64 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$d', round(d['steps_per_s'],1), d['final_loss'])") >> $O/train_speed.txt || exit 1
-  done
-done
-cat $O/train_speed.txt
-cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-timeout -k 10 180 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python -m newsrecommendationsystem_amd.train --steps 50 --batch 64 > $O/prof.log 2>&1 || { tail -5 $O/prof.log; exit 1; }
-f=$(find $O/prof -name "*kernel_stats.csv" | head -1); cp "$f" $O/train_kernel_stats.csv; head -25 $O/train_kernel_stats.csv | cut -d, -f1-4
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 || { tail -40 $O/gputests.log; exit 1; }
+tail -2 $O/gputests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d['stages_ms'])"
+timeout -k 10 900 bash profiles/run_profile.sh r5f > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
+tail -3 $O/profile.log
