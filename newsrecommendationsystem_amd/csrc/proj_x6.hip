@@ -194,7 +194,7 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
   const int t = threadIdx.x;
   // the classification blocks first (their id loads are the launch's long
   // pole; dispatched last they set its end)
-  if (b < cj.nblk) return tl::classify_block<true>(b, t, cj.rm, cj.tt, cj.dedupe, cj.compact, cj.sl);
+  if (b < cj.nblk) return tl::classify_block<true, true>(b, t, cj.rm, cj.tt, cj.dedupe, cj.compact, cj.sl);
   b -= (int)cj.nblk;
   if (nf16) {
     if (b < PACK_BLOCKS_H3) return pack_proj_h3(b, t, wn, pn);

@@ -80,10 +80,14 @@ __host__ __device__ constexpr int64_t classify_blocks(int64_t n_titles) { return
 // its bucket by the main pass) and copied. SPLIT: slot codes and block counts
 // (half A above); else one atomicAdd per bucket and one atomicMin per block
 // into the counters and the list entries directly.
-template <bool SPLIT>
+// LDS_ROWS: the compacted row ids through an LDS row per thread (the pack
+// launch's half A: 20 KB of static LDS there; -1 µs on qkv_news,
+// profiles/r5/r5zc_rowlist_clslds_ab.txt) instead of the register form.
+template <bool SPLIT, bool LDS_ROWS = false>
 __device__ __forceinline__ void classify_block(int64_t blk, int tid, const RowMap& rm, const Titles& tt, int dedupe,
                                                int compact, TitleSlots sl) {
   __shared__ int wcnt[NBK][CLS_W], wbase[NBK][CLS_W], wrep[CLS_W];
+  __shared__ __attribute__((aligned(16))) int32_t cls_rows[LDS_ROWS ? CLS_T : 1][FL];   // (this thread's row ids)
   const int64_t s = blk * CLS_T + tid;
   const int lane = tid & 63, w = tid >> 6;
   int bucket = -1;
@@ -101,9 +105,7 @@ __device__ __forceinline__ void classify_block(int64_t blk, int tid, const RowMa
       if (rm.direct) return (int32_t)(s * FL + i);
       return ((uint64_t)id[i] < (uint64_t)rm.n_rows) ? (int32_t)id[i] : -1;
     };
-    // the 20 compacted row ids in registers (static indices only: a running
-    // output index spilled the array and turned the stores into 20 scattered
-    // 4-B writes per title), stored as five 16-B writes
+    // the 20 compacted row ids, stored as five 16-B writes
     int32_t out[FL];
     uint32_t nz = 0;
 #pragma unroll
@@ -114,15 +116,38 @@ __device__ __forceinline__ void classify_block(int64_t blk, int tid, const RowMa
       const int first_pad = __ffs(~nz & ((1u << FL) - 1)) - 1;   // (-1: no padding)
       const int32_t rep_row = rm.direct ? (int32_t)(s * FL + (first_pad < 0 ? 0 : first_pad))
                                         : (rm.n_rows > 0 ? 0 : -1);
+      if constexpr (LDS_ROWS) {
+        // through this thread's LDS row: real token i goes to position
+        // popc(nz below i) (a dynamic index; in registers it would spill, and the
+        // static form is 210 selects per title)
+        int4* mine = reinterpret_cast<int4*>(cls_rows[tid]);
 #pragma unroll
-      for (int q = 0; q < FL; ++q) out[q] = q == c ? rep_row : -2;
+        for (int k = 0; k < FL / 4; ++k) {
+          const int q = 4 * k;
+          mine[k] = make_int4(q == c ? rep_row : -2, q + 1 == c ? rep_row : -2, q + 2 == c ? rep_row : -2,
+                              q + 3 == c ? rep_row : -2);
+        }
 #pragma unroll
-      for (int i = 0; i < FL; ++i) {
-        const int d = __popc(nz & ((1u << i) - 1));   // real token i's compacted position (<= i)
-        const bool real = (nz >> i) & 1;
-        const int32_t r = row(i);
+        for (int i = 0; i < FL; ++i)
+          if ((nz >> i) & 1) cls_rows[tid][__popc(nz & ((1u << i) - 1))] = row(i);
 #pragma unroll
-        for (int q = 0; q <= i; ++q) out[q] = (real && d == q) ? r : out[q];
+        for (int k = 0; k < FL / 4; ++k) {
+          const int4 v = mine[k];
+          out[4 * k] = v.x; out[4 * k + 1] = v.y; out[4 * k + 2] = v.z; out[4 * k + 3] = v.w;
+        }
+      } else {
+        // (static indices only: a running output index spilled the array and
+        // turned the stores into 20 scattered 4-B writes per title)
+#pragma unroll
+        for (int q = 0; q < FL; ++q) out[q] = q == c ? rep_row : -2;
+#pragma unroll
+        for (int i = 0; i < FL; ++i) {
+          const int d = __popc(nz & ((1u << i) - 1));   // real token i's compacted position (<= i)
+          const bool real = (nz >> i) & 1;
+          const int32_t r = row(i);
+#pragma unroll
+          for (int q = 0; q <= i; ++q) out[q] = (real && d == q) ? r : out[q];
+        }
       }
       const int le = c + (c < FL ? 1 : 0);
       bucket = (le + 3) / 4 - 1;
