@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# r5f: round-5 final build check: full GPU suite, smoke, the driver's bench
+# r5f / r5g: round-5 final build check: full GPU suite, smoke, the driver's bench
 # command, and the profile recipe (trace, traffic, SQ passes)
 set -uo pipefail
 O=gpurun_out/r5f; mkdir -p $O

@@ -1,13 +1,10 @@
 #!/usr/bin/env bash
-# r5g: kernel trace of 50 HIP training steps, HEAD vs deterministic kernels
+# r5g: HEAD (pack launch with the LDS title compaction): full GPU suite, smoke, the driver's bench command
 set -uo pipefail
-O=$PWD/gpurun_out/r5g; mkdir -p $O
-R=$PWD
-cd /tmp && export TMPDIR=/tmp
-for d in _ab/head .; do
-  n=$(basename $d); [ "$n" = "." ] && n=cur
-  (cd $R/$d && timeout -k 10 180 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_$n -o run -- python3 -m newsrecommendationsystem_amd.train --steps 50 --batch 64 > $O/prof_$n.log 2>&1) || { tail -5 $O/prof_$n.log; exit 1; }
-  f=$(find $O/prof_$n -name "*kernel_stats.csv" | head -1); cp "$f" $O/train_kernel_stats_$n.csv
-  echo "== $n"; head -22 $O/train_kernel_stats_$n.csv | cut -d, -f1-4 | cut -c1-150
-done
-rm -rf $O/prof_head $O/prof_cur
+O=gpurun_out/r5g; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 || { tail -40 $O/gputests.log; exit 1; }
+tail -2 $O/gputests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d['stages_ms'])"
