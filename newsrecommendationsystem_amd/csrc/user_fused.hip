@@ -97,6 +97,9 @@ __device__ __forceinline__ int ukpos(int k) {
 // row-list projection after dedupe); the padding row is then rep's, else the
 // user's own first padding position's.
 constexpr int UF_COPIED = 1, UF_COMPACT = 2;
+#ifndef NRMS_USER_WDEPTH
+#define NRMS_USER_WDEPTH 4
+#endif
 
 // Dispatch order of the users (with compaction): longest compacted length Le
 // first, so that the last workgroups dispatched are the short users (LPT:
@@ -490,9 +493,15 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     if constexpr (MODE == 2) {
       const uf16x8* Bq = reinterpret_cast<const uf16x8*>(WaP) + lane;
       const _Float16* t16 = reinterpret_cast<const _Float16*>(tile);
-      // W fragments one k-step ahead (an L2 round trip per k-step was the
-      // phase's latency: 6.7 k cycles even for one M-tile)
-      uf16x8 bc[NTPW][2], bn[NTPW][2];
+      // W fragments PD k-steps in flight (an L2 round trip per k-step was the
+      // phase's latency: 6.7 k cycles even for one M-tile; one k-step ahead
+      // covers one group of MFMAs, so the fewer M-tiles, the deeper: PD = 4
+      // up to two M-tiles, in the registers the larger tiles' accumulators
+      // and A fragments take)
+      // (profiles/r5/r5zf_user_wdepth_ab.txt: user_fused -0.7 us; three k-steps
+      // for three or four M-tiles took 142 VGPRs, past two workgroups per CU)
+      constexpr int PD = MT <= 2 ? NRMS_USER_WDEPTH : 2;
+      uf16x8 bq[PD][NTPW][2];
       auto load_bk = [&](int ks, uf16x8 (&dst)[NTPW][2]) __attribute__((always_inline)) {
 #pragma unroll
         for (int j = 0; j < NTPW; ++j) {
@@ -501,10 +510,12 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
           for (int pl = 0; pl < 2; ++pl) dst[j][pl] = Bq[((ks * UNT + nt) * 2 + pl) * 64];
         }
       };
-      load_bk(0, bc);
+#pragma unroll
+      for (int p = 0; p < PD - 1; ++p) load_bk(p, bq[p]);
 #pragma unroll
       for (int ks = 0; ks < UKS; ++ks) {
-        if (ks + 1 < UKS) load_bk(ks + 1, bn);
+        if (ks + PD - 1 < UKS) load_bk(ks + PD - 1, bq[(ks + PD - 1) % PD]);
+        const uf16x8 (&bc)[NTPW][2] = bq[ks % PD];
         uf16x8 a[MT][2];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
@@ -525,13 +536,6 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
           for (int mt = 0; mt < MT; ++mt)
             c[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[mt][0] * (_Float16)kF16LoScale, bc[j][0], c[mt][j],
                                                                 0, 0, 0);
-        }
-        if (ks + 1 < UKS) {
-#pragma unroll
-          for (int j = 0; j < NTPW; ++j) {
-            bc[j][0] = bn[j][0];
-            bc[j][1] = bn[j][1];
-          }
         }
       }
     } else if constexpr (MODE == 1) {
