@@ -1,13 +1,13 @@
 #!/usr/bin/env bash
-# r5h: gemm_tn slice count (deterministic partials) -- training steps/s, HEAD vs 4096 / 8192 / 16384-block targets
+# r5h: round-5 final build check (after the LDS title compaction and the UserEncoder W depth): full GPU suite, smoke, the driver's bench
+# command, and the profile recipe (trace, traffic, SQ passes)
 set -uo pipefail
 O=gpurun_out/r5h; mkdir -p $O
-NRMS_LIB_PATH=_ab/lib_tn8192.so timeout -k 10 300 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_train.py -m gpu -k "deterministic or grads_match" > $O/tests.txt 2>&1 || { tail -30 $O/tests.txt; exit 1; }
-tail -1 $O/tests.txt
-for rep in 1 2 3; do
-  for v in head tn4096 tn8192 tn16k; do
-    if [ $v = head ]; then d=_ab/head; lib=$PWD/_ab/head/newsrecommendationsystem_amd/libnrms_hip.so; else d=.; lib=$PWD/_ab/lib_$v.so; fi
-    (cd $d && NRMS_LIB_PATH=$lib timeout -k 10 120 python -m newsrecommendationsystem_amd.train --steps 300 --batch 64 2>/dev/null | tail -1 | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('$v', round(d['steps_per_s'],1), d['final_loss'])") >> $O/train_speed.txt || exit 1
-  done
-done
-cat $O/train_speed.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 || { tail -40 $O/gputests.log; exit 1; }
+tail -2 $O/gputests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d['stages_ms'])"
+timeout -k 10 900 bash profiles/run_profile.sh r5h > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
+tail -3 $O/profile.log
