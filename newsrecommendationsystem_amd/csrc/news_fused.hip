@@ -387,7 +387,11 @@ __device__ __forceinline__ floatx4 mfma4(float a, float b, floatx4 c) {
 // recheck pass runs MODE 1), context stored as fp16 planes.
 // A group of bucket NB holds 4 titles of LR = 4 NB rows each: title t's
 // compacted row p is tile row LR t + p (M = 16 NB rows, NB M-tiles).
-template <int MODE, bool EXACT>
+// CLS: the titles come classified (bucket lists and compacted rows: ts.list
+// and ts.crow set, nrms_forward's path); else every title is one 20-row slot
+// read through the RowMap. A template flag, so the per-group row staging
+// keeps no run-time branch on it (SGPRs the loop would otherwise spill).
+template <int MODE, bool EXACT, bool CLS>
 __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const float* __restrict__ qkv, int64_t ldq, RowMap rmap, TitleSet ts,
     const float* __restrict__ WaP,
@@ -448,7 +452,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   if (tid == 0) {
     int32_t n_groups = (int32_t)((n_titles + FT - 1) / FT);   // (groups < 2^27, checked at launch)
     int32_t rep = INT32_MAX;
-    if (ts.list) {
+    if constexpr (CLS) {
       rep = ts.counters[CNT_REP];
       int32_t acc = 0;
       for (int b = NBK - 1; b >= 0; --b) {
@@ -511,7 +515,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     const int32_t c = FT * g + tslot;
     const bool ok = tid < FROWS && b >= 0;
     S1 x;
-    if (!ts.list) {   // (kernel-uniform)
+    if constexpr (!CLS) {
       x.raw = c;
       x.mode = (ok && c < n_titles) ? 0 : 2;   // (n_titles <= INT32_MAX, checked at launch)
       return x;
@@ -537,7 +541,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     y.rawc = FL;
     y.rawr = 0;
     y.rawid = 0;
-    if (ts.crow) {   // (kernel-uniform)
+    if constexpr (CLS) {
       y.rawc = ts.cnt[ss];
       y.rawr = ts.crow[(int64_t)ss * FL + pslot];
     } else if (!rmap.direct && rmap.ids_a) {
@@ -550,7 +554,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     int64_t r = -2;
     if (y.s >= 0) {
       c = y.rawc;
-      if (ts.crow) r = (int64_t)y.rawr;
+      if constexpr (CLS) r = (int64_t)y.rawr;
       else if (rmap.direct || !rmap.ids_a) r = (int64_t)y.s * FL + pslot;
       else r = (uint64_t)y.rawid < (uint64_t)rmap.n_rows ? y.rawid : -1;
     }
@@ -1391,17 +1395,21 @@ int32_t launch_fused_news(const float* qkv, int64_t ldq, int64_t n_rows, const i
   const int arith = gemm_arith();
   const bool h3 = arith == NRMS_GEMM_SPLIT_F16X3;
   const bool x6 = arith != NRMS_GEMM_F32;
-  auto kern = h3 ? &fused_news_kernel<2, false> : (x6 ? &fused_news_kernel<1, false> : &fused_news_kernel<0, false>);
-  auto kern_exact = x6 ? &fused_news_kernel<1, true> : &fused_news_kernel<0, true>;
-  const size_t lds_bytes = h3 ? LDS_BYTES_H : (x6 ? LDS_BYTES_X6 : LDS_BYTES);
-  const size_t lds_bytes_exact = x6 ? LDS_BYTES_X6 : LDS_BYTES;
-  ensure_dynamic_lds(reinterpret_cast<const void*>(kern), (int)lds_bytes);
-  ensure_dynamic_lds(reinterpret_cast<const void*>(kern_exact), (int)lds_bytes_exact);
   const NewsWs z = news_ws(ws, n_titles);
   const RecheckList rl{z.counters + CNT_RECHECK, z.recheck};
   const ClassifyDecision cd =
       classify_decision(ids_a, ids_b, n_titles, n_rows, direct_rows, dedupe_setting, compact_setting);
   const bool classify = cd.classify, dedupe = cd.dedupe, compact = cd.compact;
+  auto kern = classify ? (h3 ? &fused_news_kernel<2, false, true>
+                             : (x6 ? &fused_news_kernel<1, false, true> : &fused_news_kernel<0, false, true>))
+                       : (h3 ? &fused_news_kernel<2, false, false>
+                             : (x6 ? &fused_news_kernel<1, false, false> : &fused_news_kernel<0, false, false>));
+  auto kern_exact = classify ? (x6 ? &fused_news_kernel<1, true, true> : &fused_news_kernel<0, true, true>)
+                             : (x6 ? &fused_news_kernel<1, true, false> : &fused_news_kernel<0, true, false>);
+  const size_t lds_bytes = h3 ? LDS_BYTES_H : (x6 ? LDS_BYTES_X6 : LDS_BYTES);
+  const size_t lds_bytes_exact = x6 ? LDS_BYTES_X6 : LDS_BYTES;
+  ensure_dynamic_lds(reinterpret_cast<const void*>(kern), (int)lds_bytes);
+  ensure_dynamic_lds(reinterpret_cast<const void*>(kern_exact), (int)lds_bytes_exact);
   if (preclassified && (!classify || direct_rows || !prepacked)) return NRMS_ERR_INVALID_ARG;
   const TitleSet ts{classify ? z.crow : nullptr, z.cnt, classify ? z.list : nullptr, z.counters, n_titles,
                     compact ? 0 : NBK - 1};
