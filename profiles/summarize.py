@@ -13,6 +13,7 @@ half the bytes of a wide coalesced streaming read, so read bytes are taken as
 Both include Infinity-Cache hits (memory-side request counters).
 """
 import csv
+import re
 import json
 import os
 import shutil
@@ -59,8 +60,9 @@ def stage_of(name, grid_threads, wg):
         return "user_order"
     if "fused_user" in name:
         return "user_fused"
-    if "fused_news" in name:   # the EXACT recheck launch (true) is its own line
-        return "news_recheck" if ", true>" in name else "news_fused"
+    if "fused_news" in name:   # the EXACT recheck launch (<MODE, true, ..>) is its own line
+        m = re.search(r"fused_news_kernel<\d+, (true|false)", name)
+        return "news_recheck" if m and m.group(1) == "true" else "news_fused"
     if "gather_rows_kernel" in name:
         return "gather"
     return None
