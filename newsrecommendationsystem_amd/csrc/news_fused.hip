@@ -187,7 +187,10 @@ static_assert(pk::NEWS_COUNTERS == WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS, "pack
 //                 NaN behaviour of multihead_self.py:16-20, is bitwise the
 //                 uncompacted one when all padding is trailing; an interior
 //                 id-0 token -- an OOV word, src/data_preprocess.py:134-135 --
-//                 moves to the end of the sum, fp32-rounding-level);
+//                 moves to the end of the sum, fp32-rounding-level); the
+//                 main pass (fast exp, already within rounding of the
+//                 reference's) adds the n_pad - 1 copies as one fma, the
+//                 recheck pass (rows near overflow) one at a time;
 //   context       ctx = sum_k P_k v_k with the rep's P scaled by n_pad;
 //   softmax/pool  the rep's score and context row weighted by n_pad
 //                 (additive.py:37-52).
@@ -792,8 +795,15 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
           float erep = 0.f;
 #pragma unroll
           for (int r = 0; r < 4; ++r) erep = r == rrep ? S[NB - 1][i][r] : erep;
+          if constexpr (!EXACT) {
+            // main pass: the rep's other n_pad - 1 copies in one fma (fp32
+            // rounding; the recheck pass adds them one at a time, as the
+            // uncompacted sum: profiles/r5/r5zj_news_variants_maxilp_ab.txt)
+            sum = fmaf((float)(npad > 1 ? npad - 1 : 0), erep, sum);
+          } else {
 #pragma unroll
-          for (int c = 0; c < XMAX; ++c) sum += (c + 1 < npad) ? erep : 0.f;
+            for (int c = 0; c < XMAX; ++c) sum += (c + 1 < npad) ? erep : 0.f;
+          }
           // rows near fp32 overflow (or non-finite): flagged (no branch here),
           // recomputed by the EXACT pass (RecheckList)
           if constexpr (!EXACT) recheck |= __builtin_amdgcn_ballot_w64(exp_row_needs_recheck(sum));
