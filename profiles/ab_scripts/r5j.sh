@@ -1,8 +1,13 @@
 #!/usr/bin/env bash
-# r5j: W-resident vocabulary projection (proj_wres_kernel) -- tests, then A/B against the streamed kernel
+# r5j: round-5 final build check (CLS template + rep fma + row-list chunks on the last workgroups): full GPU suite, smoke, the driver's bench
+# command, and the profile recipe (trace, traffic, SQ passes)
 set -uo pipefail
 O=gpurun_out/r5j; mkdir -p $O
-timeout -k 10 600 python -u -m pytest -x -q --timeout 280 --timeout-method thread tests/test_gpu_parity.py -m gpu -k "qkv_project or wres or plan_matches or forward or fallback" > $O/tests.txt 2>&1 || { tail -40 $O/tests.txt; exit 1; }
-tail -1 $O/tests.txt
-bash _ab/ab_env.sh "NRMS_PROJ_WRES=0" "NRMS_PROJ_WRES=1" > $O/ab.txt 2>&1 || { cat $O/ab.txt; exit 1; }
-cat $O/ab.txt
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gputests.log 2>&1 || { tail -40 $O/gputests.log; exit 1; }
+tail -2 $O/gputests.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
+tail -2 $O/smoke.log
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
+python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['ms_per_step'],d['stages_ms'])"
+timeout -k 10 900 bash profiles/run_profile.sh r5j > $O/profile.log 2>&1 || { tail -20 $O/profile.log; exit 1; }
+tail -3 $O/profile.log
