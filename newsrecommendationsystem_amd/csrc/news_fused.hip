@@ -785,7 +785,8 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         };
         // P = exp(S / sqrt(dk)) / (sum_keys + 1e-8): query 4i + x, key 4j + r.
         // Keys past Le (unused slots) are 0; the rep's other n_pad - 1 copies
-        // are added after the rep, one at a time (the uncompacted sum, bitwise).
+        // are added after the rep (recheck pass: one at a time, the
+        // uncompacted sum bitwise; main pass: one fma, below).
         auto s_exp = [&](int i) {
           float sum = 0.f;
 #pragma unroll
