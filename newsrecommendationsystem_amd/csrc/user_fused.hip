@@ -147,6 +147,14 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   constexpr int NTPW = (UNT + NW - 1) / NW;            // N-tiles per wave
   constexpr int MT = (LMAX + 15) / 16;                 // M-tiles
   extern __shared__ __attribute__((aligned(16))) float ulds[];
+  // Wave priority: 2, except 0 in the additive GEMM (below). Two workgroups
+  // share a CU; a GEMM wave waits on its W fragments from L2 between MFMA
+  // groups and gives the issue slots to the other workgroup's staging /
+  // attention / pooling waves (user_fused -1.3 %, faster 6/6 same-box;
+  // priority to the GEMM instead: -1.7 %, 3/3; over the attention alone:
+  // -1.0 %; over the softmax / pooling / scores alone: nothing;
+  // profiles/r5/r5zm_setprio_ab.txt, r5zn_user_setprio_ab.txt)
+  __builtin_amdgcn_s_setprio(2);
 #ifdef NRMS_USER_TIMING   // probe build (profiles/probes/user_phases.py): phase cycles of wave 0
   unsigned long long ut[8] = {0, 0, 0, 0, 0, 0, 0, 0}, uprev = __builtin_amdgcn_s_memtime();
 #define NRMS_U_STAMP(k)                                           \
@@ -617,6 +625,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       }
     }
   };
+  __builtin_amdgcn_s_setprio(0);
   if (w < UNT) {
     const int mte = (L + 15) / 16;
     if (mte <= 1) gemm(std::integral_constant<int, 1>{});
@@ -624,6 +633,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     else if (mte == 3) gemm(std::integral_constant<int, 3 < MT ? 3 : MT>{});
     else gemm(std::integral_constant<int, MT>{});
   }
+  __builtin_amdgcn_s_setprio(2);
   __syncthreads();
   NRMS_U_STAMP(3)   // additive GEMM + tanh·q
 
