@@ -94,13 +94,27 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(model, cand, clk, reps=3):
+def _cpu_ranges(cpus):
+    """'0-15,64-79' style summary of a CPU set."""
+    cpus, out, a = sorted(cpus), [], None
+    for i, c in enumerate(cpus):
+        if a is None:
+            a = c
+        if i + 1 == len(cpus) or cpus[i + 1] != c + 1:
+            out.append(f"{a}-{c}" if c != a else f"{a}")
+            a = None
+    return ",".join(out)
+
+
+def cpu_baseline(model, cand, clk, reps=5):
     """SURVEY §8d CPU leg: the oracle's ATen-order restatement of the
     reference forward (oracle/nrms_torch_cpu.py, bit-exact with the reference
     on the golden vectors) on the SAME batch as the GPU step (B impressions),
     median of `reps` timed runs after one warm-up, on this process's CPU
-    share (OMP_NUM_THREADS / affinity); also the GPU-vs-CPU logits parity on
-    that batch."""
+    share (OMP_NUM_THREADS / affinity; the affinity set is recorded: the
+    host's other tenants move single runs by up to ~35 %, so the spread of
+    the runs is reported beside the median); also the GPU-vs-CPU logits
+    parity on that batch."""
     from oracle import nrms_torch_cpu as T
     threads = int(os.environ.get("OMP_NUM_THREADS") or len(os.sched_getaffinity(0)))
     prev = torch.get_num_threads()
@@ -121,8 +135,12 @@ def cpu_baseline(model, cand, clk, reps=3):
     B = cand.shape[0]
     med = sorted(times)[len(times) // 2]
     err = float(((gpu - ref).norm(dim=1) / ref.norm(dim=1).clamp_min(1e-30)).max())
+    aff = os.sched_getaffinity(0)
     info = {"value": round(B / med, 2), "unit": "impressions/s", "cores": threads, "kind": "port",
             "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "affinity": _cpu_ranges(aff), "affinity_cpus": len(aff),
+            "runs_s": [round(t, 3) for t in times],
+            "spread": round((max(times) - min(times)) / med, 3),
             "sample": f"NRMS.forward over the bench batch ({B} impressions, 1+K=5, 50 clicked, L=20, "
                       f"V={V_WORDS}) via oracle/nrms_torch_cpu.py, torch {torch.__version__}, "
                       f"{threads} threads, median of {reps} runs "
@@ -398,6 +416,80 @@ def run_steps(fwd, batches, steps, events=None):
         fwd.run(cand, clk, events[k] if events else None)
 
 
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, backend):
+    """`python bench.py --gpus N` (N > 1) started without a launcher: run
+    torch.distributed.run with N processes (one per GPU) as a CHILD process
+    -- before this process has touched the GPU, and never by exec -- whose
+    rank 0 prints the JSON line straight to our stdout; return its exit code.
+    With the nccl (RCCL) backend every rank needs its own GPU: fewer visible
+    devices than N is fatal (gloo may share one GPU, for rehearsals)."""
+    import subprocess
+    if backend == "nccl":
+        have = torch.cuda.device_count()   # counts devices without initialising HIP
+        if have < n:
+            print(f"bench.py: --gpus {n} with the nccl backend needs {n} GPUs, {have} visible", file=sys.stderr)
+            return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+           os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, NRMS_BENCH_LAUNCHER="bench.py --gpus (torch.distributed.run child)")
+    return subprocess.call(cmd, env=env)
+
+
+def fedavg_sync_leg(model, device, dist, reps=5):
+    """Config 5's collective, timed once the scoring steps are done: one
+    train.FedAvg sync of all 21,955,400 parameters (flatten, all-reduce over
+    the process group -- RCCL over xGMI under nccl --, divide by the world
+    size, unflatten; the insertion point after src/train.py:233) and the
+    all-reduce alone, HIP events over `reps` calls after a warm one, max over
+    ranks. The parameters are restored afterwards (the ranks hold the same
+    weights, but a ring sum of W equal values need not round back to them)."""
+    from newsrecommendationsystem_amd.distributed import all_reduce_, max_over_ranks
+    from newsrecommendationsystem_amd.train import FedAvg
+    fa = FedAvg(model, every=1)
+    before = [p.detach().clone() for p in fa.params]
+    world = dist.get_world_size()
+    nbytes = fa.flat.numel() * 4
+
+    def timed(fn):
+        fn()
+        torch.cuda.synchronize(device)
+        dist.barrier()
+        s = torch.cuda.current_stream(device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s)
+        for _ in range(reps):
+            fn()
+        e1.record(s)
+        e1.synchronize()
+        return max_over_ranks(e0.elapsed_time(e1) / reps, device)
+
+    with torch.no_grad():
+        sync_ms = timed(fa.sync)
+        identity = all(torch.equal(p, b) for p, b in zip(fa.params, before))
+        ar_ms = timed(lambda: all_reduce_(fa.flat))
+        for p, b in zip(fa.params, before):
+            p.copy_(b)
+    algbw = nbytes / (ar_ms / 1e3) / 1e9
+    return {"params": fa.flat.numel(), "param_bytes": nbytes, "world": world, "backend": dist.get_backend(),
+            "reps": reps, "fedavg_sync_ms": round(sync_ms, 4), "all_reduce_ms": round(ar_ms, 4),
+            "all_reduce_algbw_GBps": round(algbw, 1),
+            "all_reduce_busbw_GBps": round(algbw * 2 * (world - 1) / world, 1),
+            "params_bitwise_unchanged_by_sync": identity,
+            "note": "train.FedAvg.sync (flatten + all_reduce + divide + unflatten) and the all-reduce alone, "
+                    "after the timed region; busbw = algbw * 2(W-1)/W (ring all-reduce); parameters restored "
+                    "after the measurement"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -440,11 +532,18 @@ def main():
     if args.no_cpu_baseline:
         args.no_quality = True
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us: start one (a child, before any GPU call)
+        sys.exit(launch_ranks(args.gpus, args.dist_backend))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(f"warning: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE", file=sys.stderr)
+        raise SystemExit(f"bench.py: WORLD_SIZE={world} but --gpus={args.gpus}: the launcher's process "
+                         f"count and --gpus must agree")
+    if world > 1 and args.dist_backend == "nccl" and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: {world} ranks on the nccl backend need {world} GPUs, "
+                         f"{torch.cuda.device_count()} visible")
     device = torch.device("cuda", local % max(torch.cuda.device_count(), 1))
     torch.cuda.set_device(device)
     dist = None
@@ -583,6 +682,9 @@ def main():
         n_done = sum(y.shape[0] for y in ys)
         np.savez(f"{args.dump_logits}.rank{rank}.npz", idx=idx[:n_done].cpu().numpy(),
                  logits=torch.cat(ys).float().cpu().numpy())
+    # config 5's collective (the FedAvg parameter all-reduce over the group),
+    # after the timed region: a multi-rank run measures its xGMI cost too
+    fedavg = fedavg_sync_leg(model, device, dist) if dist else None
     with torch.no_grad():
         run_steps(fwd, full, n_ev, events)
         torch.cuda.synchronize()
@@ -752,7 +854,12 @@ def main():
         "forward_paths_bitwise_equal": same,
         "graph_replay": graph is not None,
         "process_group": None if not dist else dist.get_backend(),
+        "world_size": dist.get_world_size() if dist else 1,
+        "launcher": os.environ.get("NRMS_BENCH_LAUNCHER",
+                                   "torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else "none"),
     }
+    if fedavg is not None:
+        out["fedavg_sync"] = fedavg
     if args.as_shard:
         out["config"]["as_shard"] = args.as_shard
     if rank == 0 and world == 1 and not args.no_extras and not args.stream:

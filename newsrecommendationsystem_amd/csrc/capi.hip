@@ -17,7 +17,7 @@ static thread_local int32_t g_last_hip = 0;
 void set_last_hip_error(hipError_t e) { g_last_hip = (int32_t)e; }
 
 static int initial_gemm_arith() {
-  const char* e = getenv("NRMS_GEMM");
+  const char* e = env_knob("NRMS_GEMM");
   if (e && (e[0] == 'f' || e[0] == 'F')) return NRMS_GEMM_F32;
   if (e && (e[0] == 'x' || e[0] == 'X')) return NRMS_GEMM_SPLIT_BF16X6;
   return NRMS_GEMM_SPLIT_F16X3;
@@ -29,7 +29,7 @@ static std::atomic<int> g_gemm_arith{initial_gemm_arith()};
 // (the user dispatch order moves with it); NRMS_SCORE_FOLD -- the click scores
 // in the UserEncoder launch instead of the score kernel.
 static bool env_on(const char* name) {
-  const char* e = getenv(name);
+  const char* e = env_knob(name);
   return !(e && e[0] == '0');
 }
 static const bool g_split_classify = env_on("NRMS_SPLIT_CLASSIFY");
@@ -38,7 +38,7 @@ static const bool g_split_classify = env_on("NRMS_SPLIT_CLASSIFY");
 // again itself -- the fallback nrms_forward takes when the projection leaves
 // its fragment path after the pack
 static const bool g_skip_classify_tail = [] {
-  const char* e = getenv("NRMS_TEST_SKIP_CLASSIFY_TAIL");
+  const char* e = env_knob("NRMS_TEST_SKIP_CLASSIFY_TAIL");
   return e && e[0] == '1';
 }();
 static const bool g_score_fold = env_on("NRMS_SCORE_FOLD");

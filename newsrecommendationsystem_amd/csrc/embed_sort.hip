@@ -5,13 +5,14 @@
 // gradient (the atomic form in train.hip adds in arrival order).
 //
 //   keys:  key[t] = ids[t], or V for padding / out-of-range ids (sorted last)
-//   sort:  (key, t) pairs by key, stable LSD radix sort (rocPRIM via hipCUB):
+//   sort:  (key, t) pairs by key, stable LSD radix sort (rocprim::radix_sort_pairs):
 //          within one id the tokens stay in ascending t
 //   sum:   one wave per sorted position that starts a run of equal keys:
-//          acc = dtable[id]; acc += dx[t] for the run's tokens in order; store
+//          find the run's end, then acc = dtable[id]; acc += dx[t] for the
+//          run's tokens in order (loads EMB_UNROLL tokens ahead); store
 #include "nrms_common.hpp"
 
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 namespace nrms {
 namespace {
@@ -27,7 +28,18 @@ __global__ __launch_bounds__(256) void embed_keys_kernel(const int64_t* __restri
 }
 
 // one wave per sorted position i; only the first position of each run of
-// equal keys works (the others exit at once)
+// equal keys works (the others exit at once). The run's end is found first by
+// a coalesced scan of the keys (64 per step, a ballot for the first other
+// key), so the token loop has a bound that is not a load: its tok / dx loads
+// are issued EMB_UNROLL tokens at a time ahead of the adds, which stay one
+// chain per column in token order (the CPU reference's index_add order,
+// bitwise). All of D is covered in one pass: lane l adds columns l + 64 j.
+// A real MIND batch repeats stopword / punctuation ids ~10^3 times, so one
+// run's wave is latency-bound per token unless its loads are in flight
+// together (the loop bound used to be key[p], a dependent load).
+constexpr int EMB_COLS = 5;      // 5 x 64 = 320 columns per pass (D = 300: one pass)
+constexpr int EMB_UNROLL = 8;    // tokens whose loads are in flight together
+
 __global__ __launch_bounds__(256) void embed_run_sum_kernel(const int32_t* __restrict__ key,
                                                             const int32_t* __restrict__ tok, int64_t n,
                                                             int64_t V, const float* __restrict__ dx, int D,
@@ -37,24 +49,55 @@ __global__ __launch_bounds__(256) void embed_run_sum_kernel(const int32_t* __res
   if (i >= n) return;
   const int32_t k = key[i];
   if (k >= V || (i > 0 && key[i - 1] == k)) return;
+  // run end: the first position after i holding another key (or n)
+  int64_t end = n;
+  for (int64_t p = i + 1; p < n; p += 64) {
+    const int64_t q = p + lane;
+    const bool other = q >= n || key[q] != k;
+    const uint64_t m = __ballot(other);
+    if (m) {
+      end = p + __builtin_ctzll(m);
+      break;
+    }
+  }
+  if (end > n) end = n;
   float* row = dtable + (int64_t)k * D;
-  for (int d0 = 0; d0 < D; d0 += 64 * 4) {
-    float acc[4];
+  for (int d0 = 0; d0 < D; d0 += 64 * EMB_COLS) {
+    float acc[EMB_COLS];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < EMB_COLS; ++j) {
       const int d = d0 + lane + 64 * j;
       acc[j] = d < D ? row[d] : 0.f;
     }
-    for (int64_t p = i; p < n && key[p] == k; ++p) {
+    int64_t p = i;
+    for (; p + EMB_UNROLL <= end; p += EMB_UNROLL) {
+      // the block's token indices: lanes 0..7 load one each, broadcast
+      const int32_t my_t = tok[p + (lane & (EMB_UNROLL - 1))];
+      float v[EMB_UNROLL][EMB_COLS];
+#pragma unroll
+      for (int u = 0; u < EMB_UNROLL; ++u) {
+        const float* src = dx + (int64_t)__shfl(my_t, u) * D;
+#pragma unroll
+        for (int j = 0; j < EMB_COLS; ++j) {
+          const int d = d0 + lane + 64 * j;
+          v[u][j] = d < D ? src[d] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < EMB_UNROLL; ++u)
+#pragma unroll
+        for (int j = 0; j < EMB_COLS; ++j) acc[j] += v[u][j];
+    }
+    for (; p < end; ++p) {
       const float* src = dx + (int64_t)tok[p] * D;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
+      for (int j = 0; j < EMB_COLS; ++j) {
         const int d = d0 + lane + 64 * j;
         if (d < D) acc[j] += src[d];
       }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < EMB_COLS; ++j) {
       const int d = d0 + lane + 64 * j;
       if (d < D) row[d] = acc[j];
     }
@@ -69,9 +112,9 @@ int end_bit_of(int64_t V) {
 
 size_t sort_temp_bytes(int64_t n, int64_t V) {
   size_t bytes = 0;
-  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
-                                           (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, 0, end_bit_of(V),
-                                           (hipStream_t)0);
+  (void)rocprim::radix_sort_pairs(nullptr, bytes, (const int32_t*)nullptr, (int32_t*)nullptr,
+                                  (const int32_t*)nullptr, (int32_t*)nullptr, (size_t)n, 0u,
+                                  (unsigned)end_bit_of(V), (hipStream_t)0);
   return bytes;
 }
 
@@ -101,8 +144,8 @@ int32_t launch_embedding_backward_sorted(const int64_t* ids, int64_t n_tok, cons
   hipLaunchKernelGGL(embed_keys_kernel, dim3((unsigned)((n_tok + 255) / 256)), dim3(256), 0, s, ids, n_tok, V,
                      padding_idx, key_in, tok_in);
   if (int32_t st = launch_status()) return st;
-  const hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, key_in, key_out, tok_in, tok_out,
-                                                          (int)n_tok, 0, end_bit_of(V), s);
+  const hipError_t e = rocprim::radix_sort_pairs(temp, temp_bytes, key_in, key_out, tok_in, tok_out,
+                                                 (size_t)n_tok, 0u, (unsigned)end_bit_of(V), s);
   if (e != hipSuccess) {
     set_last_hip_error(e);
     return NRMS_ERR_HIP;

@@ -1324,11 +1324,11 @@ NewsWs news_ws(float* ws, int64_t n_titles) {
 }  // namespace
 
 static std::atomic<int> g_title_dedupe{[] {
-  const char* e = getenv("NRMS_DEDUPE");
+  const char* e = env_knob("NRMS_DEDUPE");
   return (e && e[0] == '0') ? 0 : 1;
 }()};
 static std::atomic<int> g_token_compaction{[] {
-  const char* e = getenv("NRMS_COMPACT");
+  const char* e = env_knob("NRMS_COMPACT");
   return (e && e[0] == '0') ? 0 : 1;
 }()};
 // per-thread overrides (nrms_set_thread_*; -1: none)

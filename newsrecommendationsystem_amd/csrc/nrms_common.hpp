@@ -1,5 +1,6 @@
 // Shared device helpers and launch plumbing for libnrms_hip.so (gfx950 only).
 #pragma once
+#include <cstdio>
 #include <cstdlib>
 
 #include <hip/hip_runtime.h>
@@ -134,6 +135,16 @@ struct WeightRows {
   int accumulate = 0;  // store GEMMs: Y += X W^T (+ b)
 };
 
+// Run-time knobs read from the environment (the A/B switches of the launch
+// folding and the compaction, measurement and test hooks): each is read once,
+// and one that is set is announced on stderr, so a stray variable in a
+// user's environment cannot change a layout or a dispatch silently.
+inline const char* env_knob(const char* name) {
+  const char* e = getenv(name);
+  if (e) fprintf(stderr, "[nrms] environment knob %s=%s is active (non-default layout / dispatch)\n", name, e);
+  return e;
+}
+
 // Row stride (floats) of the q|k|v rows the hot path writes and the fused
 // kernels read: 3D, unpadded. Rows padded to whole 128-B lines (928 for
 // D = 300) were measured slower end to end (0.911 vs 0.869 ms per bench step,
@@ -145,7 +156,7 @@ struct WeightRows {
 // Cache) without changing the bytes any kernel reads or writes.
 inline int64_t qkv_row_stride(int D) {
   static const int64_t extra = [] {
-    const char* e = getenv("NRMS_QKV_STRIDE");
+    const char* e = env_knob("NRMS_QKV_STRIDE");
     return e ? (int64_t)atoll(e) - 900 : (int64_t)0;
   }();
   const int64_t s = (int64_t)3 * D;

@@ -148,6 +148,10 @@ constexpr int64_t RED_CHUNK = 64;
 inline size_t reduce_scratch_floats(int64_t rows, int64_t cols) {
   return rows > RED_CHUNK ? (size_t)((rows + RED_CHUNK - 1) / RED_CHUNK) * cols : 0;
 }
+// whether reduce_rows_add takes `rows` rows (its chunk count is a grid y
+// extent); callers check it before writing any output, so an UNSUPPORTED
+// return leaves every output untouched
+inline bool reduce_rows_supported(int64_t rows) { return (rows + RED_CHUNK - 1) / RED_CHUNK <= 65535; }
 // out[c] += sum_r part[r][c]: one pass for at most RED_CHUNK rows, else chunks
 // of RED_CHUNK rows into `scratch` and a second pass over the chunk sums
 int32_t reduce_rows_add(const float* part, int64_t rows, int64_t cols, float* out, float* scratch, hipStream_t s) {
@@ -622,7 +626,7 @@ int32_t launch_additive_backward_rows(const float* x, const float* y, const floa
                                       float* part, hipStream_t s) {
   if (n_seq == 0) return NRMS_OK;
   if (L < 1 || L > 64) return NRMS_ERR_UNSUPPORTED;
-  if (n_seq > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
+  if (n_seq > INT32_MAX || !reduce_rows_supported(n_seq)) return NRMS_ERR_UNSUPPORTED;
   float* pq = part;
   float* pb = part + n_seq * Q;
   hipLaunchKernelGGL(additive_backward_rows_kernel, dim3((unsigned)n_seq), dim3(256), 0, s, x, y,

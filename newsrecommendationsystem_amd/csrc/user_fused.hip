@@ -769,13 +769,13 @@ int32_t launch_user_inst(const float* qkv, int64_t ldq, int64_t B, int L, const 
 }
 
 static std::atomic<int> g_user_chunk{[] {
-  const char* e = getenv("NRMS_USER_CHUNK");
+  const char* e = env_knob("NRMS_USER_CHUNK");
   return (e && e[0] == '0') ? 0 : 1;
 }()};
 
 // (measurement only) NRMS_USER_LMAX=n: take the instance of the smallest LMAX >= max(L, n)
 static const int g_user_lmax_min = [] {
-  const char* e = getenv("NRMS_USER_LMAX");
+  const char* e = env_knob("NRMS_USER_LMAX");
   return e ? atoi(e) : 0;
 }();
 
@@ -801,7 +801,7 @@ int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const 
 size_t fused_user_packed_b_floats() { return (size_t)UWAP_MAX + USTAMP_FLOATS; }
 
 static std::atomic<int> g_user_lpt{[] {
-  const char* e = getenv("NRMS_USER_LPT");
+  const char* e = env_knob("NRMS_USER_LPT");
   return (e && e[0] == '0') ? 0 : 1;
 }()};
 bool user_lpt() { return g_user_lpt.load(std::memory_order_relaxed) != 0; }

@@ -3,8 +3,8 @@ tests/golden/gen_golden_flow.py): the eval pipeline vs the reference
 evaluate(), HIP gradients and HipAdam vs the reference training step, a
 reference checkpoint resumed on the GPU, and the raw-exp overflow boundary.
 
-Tolerances: logits / gradients normwise 1e-4 (fp32, different reduction
-orders; the W_K bias gradient is analytically zero, so rounding noise under an
+Tolerances: eval logits and news vectors normwise 1e-5 (round 6; observed
+~1e-7); gradients normwise 1e-4 (fp32, different reduction orders; the W_K bias gradient is analytically zero, so rounding noise under an
 absolute floor); metrics |delta| <= 1e-6 per impression where the logits'
 order is unambiguous, the tuple within the north star's 0.002 AUC and in fact
 1e-6 here; NaN must match NaN.
@@ -54,7 +54,7 @@ def test_hip_evaluate_matches_reference_evaluate(flow, device, max_count, gemm_m
     ref_y = flow["eval_y_pred"]
     for a, b in zip(plan.offsets[:-1], plan.offsets[1:]):
         err = np.linalg.norm(y[a:b] - ref_y[a:b]) / max(np.linalg.norm(ref_y[a:b]), 1e-30)
-        assert err < 1e-4, err
+        assert err < 1e-5, err
     np.testing.assert_allclose(metrics.cpu().numpy(), flow["eval_metrics"], rtol=0, atol=1e-6,
                                equal_nan=True)
 
@@ -160,4 +160,4 @@ def test_raw_exp_overflow_boundary_matches_reference(flow, device, gemm_mode):
         assert np.isnan(out[nan_ref]).all()
         ok = ~nan_ref
         err = np.linalg.norm(out[ok] - ref[ok], axis=1) / np.linalg.norm(ref[ok], axis=1)
-        assert err.max() < 1e-3, (mode, err.max())
+        assert err.max() < 1e-5, (mode, err.max())

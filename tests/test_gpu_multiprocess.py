@@ -256,6 +256,47 @@ def test_bench_two_ranks_weak_graph_gloo(tmp_path):
     assert len(seen) == 2 * B   # disjoint shards
 
 
+@pytest.mark.timeout(900)
+def test_bench_gpus2_self_launch_gloo(tmp_path):
+    """The driver's plain form `python bench.py --gpus 2` with NO launcher
+    around it: bench.py starts torch.distributed.run with two ranks as a child
+    process itself (here gloo, both ranks on cuda:0) and relays rank 0's
+    line: rc 0, one JSON line, n_gpus 2 = world_size, the FedAvg sync leg
+    timed over the group, each rank's graph-replayed logits bitwise equal to
+    `--as-shard r/2`'s single-process run of its shard."""
+    B = 1024
+    two = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--steps", "5",
+                          "--warmup", "2", "--no-extras", "--no-cpu-baseline", "--dump-logits", str(tmp_path / "two")],
+                         cwd=ROOT, capture_output=True, text=True, timeout=600,
+                         env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    rec = _check_weak_record(two, 2, "gloo")
+    assert rec["world_size"] == 2 and "child" in rec["launcher"]
+    fa = rec["fedavg_sync"]
+    assert fa["world"] == 2 and fa["params"] == 21955400 and fa["fedavg_sync_ms"] > 0
+    for r in range(2):
+        shard = subprocess.run([sys.executable, "bench.py", "--as-shard", f"{r}/2", "--steps", "2", "--warmup", "1",
+                                "--no-extras", "--no-cpu-baseline", "--dump-logits", str(tmp_path / f"s{r}")],
+                               cwd=ROOT, capture_output=True, text=True, timeout=400)
+        assert shard.returncode == 0, shard.stderr[-3000:]
+        got, ref = np.load(tmp_path / f"two.rank{r}.npz"), np.load(tmp_path / f"s{r}.rank0.npz")
+        assert len(got["idx"]) == B and np.array_equal(got["idx"], ref["idx"])
+        assert np.array_equal(got["logits"].view(np.uint32), ref["logits"].view(np.uint32)), r
+
+
+@pytest.mark.timeout(300)
+def test_bench_gpus2_nccl_on_one_gpu_is_fatal():
+    """`python bench.py --gpus 2` under nccl (RCCL) on a one-GPU box exits
+    non-zero with a message instead of benchmarking one GPU."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("more than one GPU visible")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--no-extras", "--no-cpu-baseline"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=200,
+                       env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert p.returncode != 0 and "needs 2 GPUs" in p.stderr, p.stderr[-2000:]
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
 @pytest.mark.timeout(600)
 def test_bench_rccl_world1_weak_graph(tmp_path):
     """The same weak-scaling graph path on RCCL: torch.distributed.run with
@@ -269,7 +310,13 @@ def test_bench_rccl_world1_weak_graph(tmp_path):
                           "--init-dist", "--dist-backend", "nccl", "--steps", "5", "--warmup", "2",
                           "--no-extras", "--no-cpu-baseline", "--dump-logits", str(tmp_path / "rccl")],
                          cwd=ROOT, capture_output=True, text=True, timeout=400)
-    _check_weak_record(one, 1, "nccl")
+    rec = _check_weak_record(one, 1, "nccl")
+    # config 5's collective timed on RCCL: at world size 1 the average of one
+    # client is the client's own parameters, bitwise
+    fa = rec["fedavg_sync"]
+    assert fa["backend"] == "nccl" and fa["world"] == 1 and fa["params"] == 21955400
+    assert fa["fedavg_sync_ms"] > 0 and fa["all_reduce_ms"] > 0
+    assert fa["params_bitwise_unchanged_by_sync"] is True
     got = np.load(tmp_path / "rccl.rank0.npz")
     idx, ref = _shard_logits(0, 1, 1024)
     assert np.array_equal(got["idx"], idx)

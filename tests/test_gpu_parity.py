@@ -1,7 +1,10 @@
 """HIP path vs the oracle / golden vectors, through the C ABI (ctypes).
 
-Tolerances: gather bit-exact; encoders and scores normwise
-||a-b||/||b|| <= 1e-3 per output vector (the fp32 MFMA path lands ~1e-6).
+Tolerances: gather bit-exact; encoders and scores normwise ||a-b||/||b||
+<= TOL = 1e-5 per output vector. SURVEY §8d / the north star allow 1e-3
+(SPEC_TOL); the kernels land at 2-5e-7 against the fp32 golden and the fp64
+oracle, so the assertions sit at 1e-5 (round 6): a lost split plane or a
+wrong scale (errors of 1e-4 and up) fails them.
 """
 import ctypes
 
@@ -14,7 +17,8 @@ from oracle import weights as W
 
 pytestmark = pytest.mark.gpu
 
-TOL = 1e-3
+SPEC_TOL = 1e-3   # SURVEY §8d / north_star: "within 1e-3 rel fp32"
+TOL = 1e-5        # what the assertions hold the kernels to (observed 2-5e-7)
 
 
 def _module(state, V, device, **knobs):
@@ -173,7 +177,7 @@ def test_prediction_golden(golden, gold_model, device):
     with torch.no_grad():
         out = _np(gold_model.get_prediction(nv, uv))
     assert out.shape == (7,)
-    assert np.abs(out - golden["pred_out"]).max() <= 1e-4 * np.abs(golden["pred_out"]).max()
+    assert np.abs(out - golden["pred_out"]).max() <= TOL * np.abs(golden["pred_out"]).max()
 
 
 def test_raw_exp_overflow_nan(golden, golden_state, device, gemm_mode):
@@ -584,13 +588,16 @@ def test_bench_batch_slice_gemm_arith_vs_fp64(device):
     model: N(0,1) embedding, V = 70,976; the first 128 impressions of the
     config-4 stream's rank-0 shard) scored through nrms_forward under each
     GEMM arithmetic, against the fp64 oracle: every arithmetic's worst row
-    within 1e-5 (SURVEY §8d allows 1e-3), and f16x3 (the bench default) and
+    within 5e-6 (SURVEY §8d allows 1e-3), and f16x3 (the bench default) and
     x6 at the f32 forward's error level: their MEAN row error within 2x the
     f32 forward's. (Until round 5 this compared the max over the 128 rows,
     one row's rounding: the main pass's rep fma made the f32 forward more
     accurate, mean 9.2e-7 -> 6.5e-7, and x6's worst row moved 2.6e-6 ->
     3.3e-6 at 128 rows but 4.9e-6 -> 4.7e-6 at 512, its mean +1 %;
-    profiles/r5/r5zl_rep_fma_arith_err.txt, tests/arith_err_probe.py.)"""
+    profiles/r5/r5zl_rep_fma_arith_err.txt, tests/arith_err_probe.py. That
+    was a relaxation made to fit a result; round 6 keeps a worst-row bound
+    beside the mean: each split arithmetic's worst row within 3x the f32
+    forward's worst row.)"""
     import bench
     from newsrecommendationsystem_amd import _native as N
     from newsrecommendationsystem_amd import stream as S
@@ -607,9 +614,13 @@ def test_bench_batch_slice_gemm_arith_vs_fp64(device):
         e = O.normwise_rel_err(y, ref)
         errs[name] = (float(e.max()), float(e.mean()))
     for name in ("f32", "x6", "f16x3"):
-        assert errs[name][0] < 1e-5, errs
+        assert errs[name][0] < 5e-6, errs
     for name in ("x6", "f16x3"):
         assert errs[name][1] <= 2 * errs["f32"][1], errs
+        # and the outlier rows stay bounded next to the mean (the
+        # round-5 change to a mean-row comparison was a relaxation, so a
+        # worst-row bound is kept beside it)
+        assert errs[name][0] <= 3 * errs["f32"][0] + 1e-7, errs
 
 
 def _attention_pool(qkv, ldq, ids, w, device):
@@ -890,7 +901,7 @@ def test_config2_news_encoder_100k_titles(device, gemm_mode):
     """BASELINE config 2 at full size (100,000 titles x 20 tokens, V = 70,976,
     N(0,1) table): folded == direct within fp32 rounding (normwise 1e-5),
     encoding in two halves == one call bitwise, and a 512-title sample
-    against the fp64 oracle (normwise 1e-3 per vector)."""
+    against the fp64 oracle (normwise TOL per vector)."""
     from newsrecommendationsystem_amd import _native as N
     V, n = 70976, 100_000
     sd = W.nrms_state(8, V)
@@ -909,7 +920,7 @@ def test_config2_news_encoder_100k_titles(device, gemm_mode):
     assert rel < 1e-5, float(rel)
     pick = np.sort(W.randint(8, 501, (512,), 0, n))
     ref = O.news_encode(titles.numpy()[pick], sd, np.float64)
-    assert O.normwise_rel_err(_np(folded)[pick], ref).max() < 1e-3
+    assert O.normwise_rel_err(_np(folded)[pick], ref).max() < TOL
 
 
 @pytest.mark.parametrize("pad_frac", [0.0, 0.45, 1.0])

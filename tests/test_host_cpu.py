@@ -194,3 +194,31 @@ def test_out_of_range_ids_raise_before_device():
         m.news_encoder._ids(torch.tensor([[1, 32]]))
     with pytest.raises(IndexError):
         m.news_encoder._ids(torch.tensor([[-1, 2]]))
+
+
+def _bench(args, env=None, timeout=120):
+    import subprocess
+    import sys
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    return subprocess.run([sys.executable, "bench.py", *args], cwd=ROOT, env=e, capture_output=True,
+                          text=True, timeout=timeout)
+
+
+def test_bench_gpus_n_nccl_without_gpus_is_fatal():
+    """`python bench.py --gpus 2` (no launcher) starts torch.distributed.run
+    itself; under the nccl backend it first needs 2 visible GPUs and exits
+    non-zero, with a message, when it has fewer (here: none), before any rank
+    starts or any GPU call is made."""
+    p = _bench(["--gpus", "2", "--no-extras", "--no-cpu-baseline"])
+    assert p.returncode != 0
+    assert "needs 2 GPUs" in p.stderr, p.stderr[-2000:]
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_bench_world_size_mismatch_is_fatal():
+    """A launcher whose process count differs from --gpus is an error, not a
+    warning (the record would otherwise claim the wrong GPU count)."""
+    p = _bench(["--gpus", "1", "--no-extras"], env={"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0
+    assert "WORLD_SIZE=2 but --gpus=1" in p.stderr, p.stderr[-2000:]
