@@ -302,7 +302,12 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
 #pragma unroll
     for (int j = 0; j < AP; ++j) {
       const int c4 = aq + TPR * j < PK / 4 ? aq + TPR * j : PK / 4 - 1;   // (pieces past the row: unused)
+#ifdef NRMS_PX_NT_A   // probe: A rows as streaming loads (keep the W planes in L2)
+      const floatx4 v = __builtin_nontemporal_load(reinterpret_cast<const floatx4*>(src + 4 * c4));
+      ra[j] = make_float4(v[0], v[1], v[2], v[3]);
+#else
       ra[j] = *reinterpret_cast<const float4*>(src + 4 * c4);
+#endif
     }
   };
   auto store_a = [&](int64_t o) __attribute__((always_inline)) {

@@ -228,14 +228,43 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     }
   };
   // CHUNKED (the 512-thread, 80-KB instance for histories of 33..50 titles,
-  // two workgroups per CU): the K|V rows are staged KVR at a time (the keys in
-  // order, each chunk behind a barrier), and a user with more (head, query)
-  // tasks than threads runs them in two passes (the first pass's context kept
-  // in registers): the same per-task arithmetic in the same key order as the
-  // whole-tile instances.
+  // two workgroups per CU): a user whose (head, query) tasks fit the threads
+  // (33, 34 titles) stages its K|V rows KVR at a time (the keys in order, each
+  // chunk behind a barrier); a user with more tasks than threads (35..50
+  // titles) runs them in two passes split by HEAD (round 6): heads 0..7, then
+  // 8..14, each pass staging the K|V columns of its heads for all L keys
+  // (1,280-B rows, 64 KB at 50 keys), so every K|V byte is staged once (the
+  // round-5 passes split by task index re-staged both key chunks in the
+  // second pass: traffic 1.44x its floor) and the first pass's context is
+  // kept in registers. Either way each task runs the whole-tile instances'
+  // arithmetic over the keys in the same order: bitwise their results.
+  constexpr int HS_H = 8;                      // heads of the first pass (head split)
+  constexpr int HS_W = HS_H * UDK;             // K (and V) floats of a staged row
+  constexpr int HS_RS = 2 * HS_W;              // staged row: K | V of the pass's heads
+  static_assert(!CHUNKED || (HS_H * LMAX <= NT && (UH - HS_H) * LMAX <= NT), "one pass per head group");
+  static_assert(!CHUNKED || LMAX * HS_RS <= KVR * URS, "a head group's K|V fits the tile");
   const int ntask = UH * L;
   const int npass = CHUNKED ? (ntask + NT - 1) / NT : 1;    // (workgroup-uniform)
-  const int nchunk = CHUNKED ? (L + KVR - 1) / KVR : 1;
+  const bool hsplit = CHUNKED && npass > 1;                 // two passes, split by head
+  const int nchunk = CHUNKED && !hsplit ? (L + KVR - 1) / KVR : 1;
+  const int tb = hsplit ? HS_H * L : NT;                    // the second pass's first task
+  // K|V columns of heads hb .. hb + HS_H - 1 of rows 0 .. nr - 1 (head split):
+  // 80 16-B pieces per row, K's then V's; the 16th head slot of the second
+  // pass does not exist and re-reads the row's first piece (never used)
+  auto stage_heads = [&](int hb, int nr) __attribute__((always_inline)) {
+    constexpr int PPR = HS_RS / 4, PPS = HS_W / 4;   // pieces per row / per section
+    const int np = nr * PPR;
+    for (int p = w; p < (np + 63) >> 6; p += NT / 64) {
+      int g = (p << 6) + lane;
+      g = g < np ? g : np - 1;
+      const int i = g / PPR, c = g - i * PPR;
+      const int sec = c >= PPS ? 1 : 0, cc = c - sec * PPS;
+      const float* src = row(i) + (1 + sec) * UD + UDK * hb + 4 * cc;
+      src = hb + cc / (UDK / 4) < UH ? src : row(i) + UD;
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
+                                       (__attribute__((address_space(3))) void*)(tile + (p << 8)), 16, 0, 0);
+    }
+  };
   static_assert(!CHUNKED || UH * LMAX <= 2 * NT, "at most two task passes");
   static_assert(MODE != 2 || UNT * 64 + 64 + 64 >= UH * LMAX, "per-thread max slots before rexp");
   // exp(d / sqrt(d_k)) as v_exp_f32(d · log2(e) / sqrt(d_k)), as the news kernel
@@ -246,9 +275,13 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   [[maybe_unused]] float acc0[UDK];   // CHUNKED, two passes: the first pass's context
   float mrow = 0.f, mrow0 = 0.f;      // MODE 2: max |ctx| of this thread's task (per pass)
   for (int pass = 0; pass < npass; ++pass) {
-    const int task = tid + pass * NT;
-    const bool has = task < ntask;
+    const int task = tb * pass + tid;
+    const bool has = task < ntask && (!hsplit || pass > 0 || tid < tb);
     const int h = has ? task / L : 0, qi = has ? task - h * L : 0;
+    // head h's K and V slices within a staged row (stride krs floats)
+    const int krs = hsplit ? HS_RS : URS;
+    const int kofs = hsplit ? UDK * (h - HS_H * pass) : UDK * h;
+    const int vofs = hsplit ? HS_W + UDK * (h - HS_H * pass) : UD + UDK * h;
     {
       const float4* qp = reinterpret_cast<const float4*>(row(qi) + UDK * h);
 #pragma unroll
@@ -260,9 +293,9 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     // packed FP32 (v_pk_fma_f32, two FMAs per lane per instruction): the dot
     // product as even / odd partial sums added at the end, the context update
     // elementwise (the same FMAs as the scalar form): user_fused -1.3 us
-    // (profiles/r4o_user_pk_fma_ab.txt). kv: the K|V row (K at kv, V at kv + UD).
-    auto dot = [&](const float* kv) __attribute__((always_inline)) {
-      const float4* kr = reinterpret_cast<const float4*>(kv + UDK * h);
+    // (profiles/r4o_user_pk_fma_ab.txt). kp / vp: head h's K / V slice of a key.
+    auto dot = [&](const float* kp) __attribute__((always_inline)) {
+      const float4* kr = reinterpret_cast<const float4*>(kp);
       f2 d = f2{0.f, 0.f};
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
@@ -272,8 +305,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       }
       return d.x + d.y;
     };
-    auto axpy = [&](float a, const float* kv) __attribute__((always_inline)) {
-      const float4* vr = reinterpret_cast<const float4*>(kv + UD + UDK * h);
+    auto axpy = [&](float a, const float* vp) __attribute__((always_inline)) {
+      const float4* vr = reinterpret_cast<const float4*>(vp);
       const f2 a2 = f2{a, a};
 #pragma unroll
       for (int t = 0; t < UDK / 4; ++t) {
@@ -296,17 +329,18 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     for (int c = 0; c < nchunk; ++c) {
       const int kb = c * KVR, ke = CHUNKED ? (L < kb + KVR ? L : kb + KVR) : L;
       if (CHUNKED && (pass > 0 || c > 0)) __syncthreads();   // the previous chunk's readers are done
-      stage(kb, ke - kb);
+      if (hsplit) stage_heads(HS_H * pass, L);
+      else stage(kb, ke - kb);
       __syncthreads();
       if (c == 0 && pass == 0) { NRMS_U_STAMP(0) }   // K|V staged
       if (has) {
-        const float* kt = tile - (int64_t)kb * URS;   // key j's K|V row: kt + j URS
+        const float* kt = tile - (int64_t)kb * krs;   // key j's staged row: kt + j krs
         for (int j0 = kb; j0 < ke; j0 += 4) {
           float e[4];
 #pragma unroll
           for (int u = 0; u < 4; ++u) {
             const int j = j0 + u;
-            e[u] = j < ke ? __builtin_amdgcn_exp2f(dot(kt + (j < ke ? j : ke - 1) * URS) * rs) : 0.f;
+            e[u] = j < ke ? __builtin_amdgcn_exp2f(dot(kt + (j < ke ? j : ke - 1) * krs + kofs) * rs) : 0.f;
           }
           if (j0 == 0) {
             for (int cc = 0; cc < m0; ++cc) sum += e[0];   // (row 0's multiplicity)
@@ -318,7 +352,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
           sum += e[2];
           sum += e[3];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) axpy(e[u], kt + (j0 + u < ke ? j0 + u : ke - 1) * URS);
+          for (int u = 0; u < 4; ++u) axpy(e[u], kt + (j0 + u < ke ? j0 + u : ke - 1) * krs + vofs);
         }
       }
     }
@@ -340,7 +374,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
         auto kvr = [&](int j) -> const float* { return CHUNKED ? row(j) + UD : tile + j * URS; };
         sum = 0.f;
         for (int j = 0; j < L; ++j) {
-          const float x = ref_exp(dot(kvr(j)), sqrt_dk);
+          const float x = ref_exp(dot(kvr(j) + UDK * h), sqrt_dk);
           if (j == 0)
             for (int cc = 0; cc < m0; ++cc) sum += x;
           else
@@ -350,9 +384,9 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
 #pragma unroll
         for (int t = 0; t < UDK; ++t) acc[t] = 0.f;
         for (int j = 0; j < L; ++j) {
-          float a = ref_exp(dot(kvr(j)), sqrt_dk) * inv;
+          float a = ref_exp(dot(kvr(j) + UDK * h), sqrt_dk) * inv;
           if (j == 0 && m0 > 1) a *= (float)m0;
-          axpy(a, kvr(j));
+          axpy(a, kvr(j) + UD + UDK * h);
         }
       }
       if constexpr (MODE == 2) {
@@ -388,9 +422,12 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   const int h = tid < ntask ? tid / L : 0, qi = tid < ntask ? tid - h * L : 0;   // (the first pass's task)
   const bool has = tid < ntask;
   if constexpr (MODE == 2) {
+    // (CHUNKED: the first pass's tasks are 0 .. tb - 1, the second pass's tb ..)
+    [[maybe_unused]] const bool has0 = hsplit ? tid < tb : tid < ntask;
+    [[maybe_unused]] const bool has1 = npass > 1 && tb + tid < ntask;
     if constexpr (CHUNKED) {
-      if (has) part[tid] = npass > 1 ? mrow0 : mrow;
-      if (npass > 1 && tid + NT < ntask) part[tid + NT] = mrow;
+      if (has0) part[tid] = npass > 1 ? mrow0 : mrow;
+      if (has1) part[tb + tid] = mrow;
       __syncthreads();
     }
     // three fp16 planes per row (hi | lo | r), in the MODE 1 positions
@@ -420,8 +457,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     };
     if constexpr (CHUNKED) {
       if (npass > 1) {
-        if (has) write_ctx(tid, acc0);
-        if (tid + NT < ntask) write_ctx(tid + NT, acc);
+        if (has0) write_ctx(tid, acc0);
+        if (has1) write_ctx(tb + tid, acc);
       } else if (has) {
         write_ctx(tid, acc);
       }

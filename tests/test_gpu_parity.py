@@ -1194,3 +1194,28 @@ def test_forward_classification_fallback_without_tail_jobs():
                        timeout=300)
     assert r.returncode == 0 and "FALLBACK_OK" in r.stdout, r.stderr[-3000:]
 
+
+
+def test_user_head_split_passes_bitwise(tmp_path):
+    """The chunked UserEncoder instance (512 threads, two workgroups per CU)
+    runs users of 35..50 titles in two passes split by head, each staging its
+    heads' K|V columns for all keys once (round 6); users of 33, 34 titles in
+    one pass over two key chunks. Every (head, query) task sums the same keys
+    in the same order as the 832-thread whole-tile instance, so the user
+    vectors and the forward's logits are bitwise those of NRMS_USER_CHUNK=0
+    (including rows that take the recheck path)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for chunk in ("0", "1"):
+        env = dict(os.environ, NRMS_USER_CHUNK=chunk)
+        p = subprocess.run([sys.executable, os.path.join(root, "tests", "user_chunk_worker.py"),
+                            str(tmp_path / f"c{chunk}.npz")], env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        outs[chunk] = np.load(tmp_path / f"c{chunk}.npz")
+    for k in ("uv", "logits"):
+        a, b = outs["0"][k], outs["1"][k]
+        assert np.isfinite(b).any()
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
