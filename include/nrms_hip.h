@@ -419,8 +419,11 @@ int32_t nrms_embedding_backward(const int64_t* ids, int64_t n_tok, const float* 
                                 hipStream_t stream);
 
 /* (ABI 8) The same gradient, deterministic: the tokens are sorted by id (a
- * stable radix sort) and each row's contributions added in token order, the
- * order of the CPU reference's index_add; bitwise reproducible. Workspace:
+ * stable radix sort) and each row's contributions added in a fixed order --
+ * token order for an id with at most 256 tokens (the CPU reference's
+ * index_add order, bitwise), and for a longer run sums of 64-token segments
+ * (each in token order) added in segment order (round 6: parallel; within
+ * fp32 rounding of index_add). Bitwise reproducible. Workspace:
  * nrms_embedding_backward_workspace_size(n_tok, V) bytes; n_tok, V < 2^31. */
 size_t nrms_embedding_backward_workspace_size(int64_t n_tok, int64_t V);
 int32_t nrms_embedding_backward_ws(const int64_t* ids, int64_t n_tok, const float* dx, int64_t V,

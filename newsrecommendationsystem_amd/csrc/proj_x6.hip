@@ -244,13 +244,33 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
   int64_t* orow = reinterpret_cast<int64_t*>(As + PM * PRB);   // output row offset (-1: no row)
   int32_t* erow = reinterpret_cast<int32_t*>(orow + PM);       // H3: row exponent ea - 11
 
+#ifdef NRMS_PX_SC1
+  // (probe) the output rows through a buffer resource with sc1 stores (the
+  // line leaves the XCD's L2 once written: the W planes are not evicted by
+  // the 263-MB output stream); rows past M, columns past N and (SCATTER) ids
+  // past the capacity M get an out-of-range offset (dropped by the hardware)
+  const uint64_t y_bytes = (uint64_t)M * (uint64_t)ldy * 4;
+  const bool sc1 = y_bytes + 64 < 0xFFFFFF00ull;   // (workgroup-uniform)
+  const int64_t m_cap = M;
+  const __amdgpu_buffer_rsrc_t yrs = __builtin_amdgcn_make_buffer_rsrc(Y, 0, sc1 ? (int)y_bytes : 0, 0x00020000);
+#endif
   if constexpr (SCATTER) {
     const int64_t mc = *m_dev;
     M = mc < M ? mc : M;
   }
   const int64_t n_items = (M + PM - 1) / PM * PNR;
+#ifdef NRMS_PX_XCD
+  // (probe) XCD-major workgroup order: workgroups b, b + 8, .. (one XCD) take
+  // consecutive item ranges, so a row tile split between two workgroups is
+  // staged twice within one L2
+  const int64_t lb = (gridDim.x % 8 == 0) ? (int64_t)(blockIdx.x % 8) * (gridDim.x / 8) + blockIdx.x / 8
+                                          : (int64_t)blockIdx.x;
+  const int64_t i0 = lb * n_items / gridDim.x;
+  const int64_t i1 = (lb + 1) * n_items / gridDim.x;
+#else
   const int64_t i0 = (int64_t)blockIdx.x * n_items / gridDim.x;
   const int64_t i1 = ((int64_t)blockIdx.x + 1) * n_items / gridDim.x;
+#endif
   const bool tail = tj.sc.slot || tj.uo.pad;
   if (i0 >= i1) {
     if (tail) tl::run_tail_jobs<NTH>(tj, threadIdx.x);
@@ -511,10 +531,16 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
       // immediate offsets; tiles past N skipped, columns past N of the last masked.
       float* base[PMT];
       int ea[PMT];   // H3: row exponent - 11
+#ifdef NRMS_PX_SC1
+      uint32_t yoff[PMT];   // byte offsets into Y (0xFFFFFFF0: dropped)
+#endif
 #pragma unroll
       for (int mt = 0; mt < PMT; ++mt) {
         const int64_t o = orow[16 * mt + lm];
         base[mt] = (o >= 0 ? Y + o : trash) + 16 * t0 + 4 * kq;
+#ifdef NRMS_PX_SC1
+        yoff[mt] = (o >= 0 && o < m_cap * ldy) ? (uint32_t)((o + 16 * t0 + 4 * kq) * 4) : 0xFFFFFFF0u;
+#endif
         if constexpr (H3) ea[mt] = erow[16 * mt + lm];
       }
       auto store_tile = [&](int j) __attribute__((always_inline)) {
@@ -536,6 +562,15 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
           }
 #ifdef NRMS_PX_NOSTORE   // probe: the epilogue without its stores
           if (v.x == 12345.f) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
+#elif defined(NRMS_PX_SC1)
+          if (sc1) {
+            typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+            const uint32_t off =
+                (yoff[mt] != 0xFFFFFFF0u && (full || 16 * (t0 + j) + 4 * kq < PN)) ? yoff[mt] + 64u * j : 0xFFFFFFF0u;
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, v), yrs, off, 0, 16 /* sc1 */);
+          } else if (full || 16 * (t0 + j) + 4 * kq < PN) {
+            *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;
+          }
 #else
           // (non-temporal stores: qkv_news 0.26 vs 0.16 ms, profiles/r4q_proj_store_waves_ab.txt)
           if (full || 16 * (t0 + j) + 4 * kq < PN) *reinterpret_cast<float4*>(base[mt] + 16 * j) = v;

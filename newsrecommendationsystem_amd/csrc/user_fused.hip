@@ -236,7 +236,8 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   // (1,280-B rows, 64 KB at 50 keys), so every K|V byte is staged once (the
   // round-5 passes split by task index re-staged both key chunks in the
   // second pass: traffic 1.44x its floor) and the first pass's context is
-  // kept in registers. Either way each task runs the whole-tile instances'
+  // kept in registers. (At 49, 50 titles the head split leaves one more
+  // partly filled wave than the task-index split, which those users keep.) Either way each task runs the whole-tile instances'
   // arithmetic over the keys in the same order: bitwise their results.
   constexpr int HS_H = 8;                      // heads of the first pass (head split)
   constexpr int HS_W = HS_H * UDK;             // K (and V) floats of a staged row
@@ -245,7 +246,11 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   static_assert(!CHUNKED || LMAX * HS_RS <= KVR * URS, "a head group's K|V fits the tile");
   const int ntask = UH * L;
   const int npass = CHUNKED ? (ntask + NT - 1) / NT : 1;    // (workgroup-uniform)
-  const bool hsplit = CHUNKED && npass > 1;                 // two passes, split by head
+  // two passes split by head, unless that leaves more partly filled waves
+  // than the split by task index (49, 50 titles: 7 + 6 against 8 + 4 waves;
+  // same-box A/B, profiles/r6/r6c_user_head_split_ab.txt)
+  const bool hsplit = CHUNKED && npass > 1 &&
+                      (HS_H * L + 63) / 64 + ((UH - HS_H) * L + 63) / 64 <= NT / 64 + (ntask - NT + 63) / 64;
   const int nchunk = CHUNKED && !hsplit ? (L + KVR - 1) / KVR : 1;
   const int tb = hsplit ? HS_H * L : NT;                    // the second pass's first task
   // K|V columns of heads hb .. hb + HS_H - 1 of rows 0 .. nr - 1 (head split):
@@ -327,7 +332,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     // rounding). No exp is kept, so the work is ~L, not LMAX, keys per query.
     float sum = 0.f;
     for (int c = 0; c < nchunk; ++c) {
-      const int kb = c * KVR, ke = CHUNKED ? (L < kb + KVR ? L : kb + KVR) : L;
+      const int kb = c * KVR, ke = CHUNKED && !hsplit ? (L < kb + KVR ? L : kb + KVR) : L;
       if (CHUNKED && (pass > 0 || c > 0)) __syncthreads();   // the previous chunk's readers are done
       if (hsplit) stage_heads(HS_H * pass, L);
       else stage(kb, ke - kb);

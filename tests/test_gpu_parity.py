@@ -1201,9 +1201,14 @@ def test_user_head_split_passes_bitwise(tmp_path):
     runs users of 35..50 titles in two passes split by head, each staging its
     heads' K|V columns for all keys once (round 6); users of 33, 34 titles in
     one pass over two key chunks. Every (head, query) task sums the same keys
-    in the same order as the 832-thread whole-tile instance, so the user
-    vectors and the forward's logits are bitwise those of NRMS_USER_CHUNK=0
-    (including rows that take the recheck path)."""
+    in the same order as the 832-thread whole-tile instance (NRMS_USER_CHUNK=0),
+    so up to 39 rows, where both keep the context as three fp16 planes, the
+    user vectors are bitwise equal (34: key chunks; 38: head split; rows that
+    take the recheck path included). (49, 50 rows keep the round-5 split by
+    task index.) Past 39 rows the chunked instance packs
+    the context as two planes (22 bits, the additive GEMM's operands) and the
+    pooling rebuilds it from those: 50 rows and the bench slice's logits agree
+    within fp32-level rounding (normwise < 1e-6)."""
     import os
     import subprocess
     import sys
@@ -1215,7 +1220,12 @@ def test_user_head_split_passes_bitwise(tmp_path):
                             str(tmp_path / f"c{chunk}.npz")], env=env, capture_output=True, text=True, timeout=300)
         assert p.returncode == 0, p.stderr[-3000:]
         outs[chunk] = np.load(tmp_path / f"c{chunk}.npz")
-    for k in ("uv", "logits"):
+    for k in ("uv34", "uv38"):
         a, b = outs["0"][k], outs["1"][k]
         assert np.isfinite(b).any()
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
+    for k in ("uv50", "logits"):
+        a, b = outs["0"][k].astype(np.float64), outs["1"][k].astype(np.float64)
+        assert np.array_equal(np.isnan(a), np.isnan(b)), k
+        ok = ~np.isnan(a).any(axis=1)
+        assert O.normwise_rel_err(b[ok], a[ok]).max() < 1e-6, k

@@ -3,10 +3,11 @@ the UserEncoder outputs of one library configuration (the environment picks
 the instance: NRMS_USER_CHUNK=0 -> the 832-thread whole-tile instance, else
 the 512-thread chunked / head-split one), saved to argv[1] (.npz).
 
-  get_user_vector on [64, 50, 300] inputs (every user 50 rows: two task
-  passes), scaled so some rows take the recheck path, and nrms_forward
-  logits on a 256-impression slice of the bench batch (compacted lengths
-  1..50)."""
+  get_user_vector on [64, L, 300] inputs for L = 34 (one pass over two key
+  chunks), 38 (two passes split by head) and 50 (two passes, the context
+  packed as two planes), scaled so some rows take the recheck path, and
+  nrms_forward logits on a 256-impression slice of the bench batch
+  (compacted lengths 1..50)."""
 import os
 import sys
 
@@ -23,16 +24,18 @@ from newsrecommendationsystem_amd import stream as S  # noqa: E402
 def main(out):
     dev = torch.device("cuda:0")
     model = bench.build_model(dev)
-    g = torch.Generator(device="cpu").manual_seed(4)
-    x = torch.randn(64, 50, 300, generator=g)
-    x[::7] *= 30.0                      # large scores: rows near fp32 overflow take the recheck path
-    x[3, :20] = 0.0                     # left padding
+    res = {}
     with torch.no_grad():
-        uv = model.get_user_vector(x.to(dev)).cpu().numpy()
+        for L in (34, 38, 50):
+            g = torch.Generator(device="cpu").manual_seed(4 + L)
+            x = torch.randn(64, L, 300, generator=g)
+            x[::7] *= 30.0                      # large scores: rows near fp32 overflow take the recheck path
+            x[3, :20] = 0.0                     # left padding
+            res[f"uv{L}"] = model.get_user_vector(x.to(dev)).cpu().numpy()
         idx = bench.stream_impressions(0, 1, 256, dev)
         cand, clk = S.batch(0, idx, bench.V_WORDS)
-        y = model.forward_ids(cand, clk).cpu().numpy()
-    np.savez(out, uv=uv, logits=y)
+        res["logits"] = model.forward_ids(cand, clk).cpu().numpy()
+    np.savez(out, **res)
 
 
 if __name__ == "__main__":
