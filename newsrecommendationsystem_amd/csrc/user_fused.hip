@@ -97,6 +97,10 @@ __device__ __forceinline__ int ukpos(int k) {
 // row-list projection after dedupe); the padding row is then rep's, else the
 // user's own first padding position's.
 constexpr int UF_COPIED = 1, UF_COMPACT = 2;
+// UF_TASK_SPLIT: the chunked instance's two passes split by task index (the
+// round-5 form) even where the head split adds no wave (NRMS_USER_HSPLIT=0:
+// the test that the head split changes no bit)
+constexpr int UF_TASK_SPLIT = 4;
 #ifndef NRMS_USER_WDEPTH
 #define NRMS_USER_WDEPTH 4
 #endif
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   // two passes split by head, unless that leaves more partly filled waves
   // than the split by task index (49, 50 titles: 7 + 6 against 8 + 4 waves;
   // same-box A/B, profiles/r6/r6c_user_head_split_ab.txt)
-  const bool hsplit = CHUNKED && npass > 1 &&
+  const bool hsplit = CHUNKED && npass > 1 && !(uflags & UF_TASK_SPLIT) &&
                       (HS_H * L + 63) / 64 + ((UH - HS_H) * L + 63) / 64 <= NT / 64 + (ntask - NT + 63) / 64;
   const int nchunk = CHUNKED && !hsplit ? (L + KVR - 1) / KVR : 1;
   const int tb = hsplit ? HS_H * L : NT;                    // the second pass's first task
@@ -842,6 +846,11 @@ int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const 
 
 size_t fused_user_packed_b_floats() { return (size_t)UWAP_MAX + USTAMP_FLOATS; }
 
+static std::atomic<int> g_user_hsplit{[] {
+  const char* e = env_knob("NRMS_USER_HSPLIT");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
+
 static std::atomic<int> g_user_lpt{[] {
   const char* e = env_knob("NRMS_USER_LPT");
   return (e && e[0] == '0') ? 0 : 1;
@@ -859,7 +868,8 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
   const PaddingGroups pg = pgp ? *pgp : PaddingGroups{nullptr, nullptr, nullptr};
   if (compact && (!pgp || L > 64 || B * L > INT32_MAX)) return NRMS_ERR_UNSUPPORTED;
   if (copied && !pgp) return NRMS_ERR_INVALID_ARG;
-  const int uflags = (copied ? UF_COPIED : 0) | (compact ? UF_COMPACT : 0);
+  const int uflags = (copied ? UF_COPIED : 0) | (compact ? UF_COMPACT : 0) |
+                     (g_user_hsplit.load(std::memory_order_relaxed) ? 0 : UF_TASK_SPLIT);
   if (B == 0) return NRMS_OK;
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16 || ldq < 3 * UD || ldq % 4)

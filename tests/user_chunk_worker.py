@@ -1,7 +1,7 @@
 """Child process of tests/test_gpu_parity.py::test_user_head_split_passes_bitwise:
 the UserEncoder outputs of one library configuration (the environment picks
-the instance: NRMS_USER_CHUNK=0 -> the 832-thread whole-tile instance, else
-the 512-thread chunked / head-split one), saved to argv[1] (.npz).
+the form: NRMS_USER_HSPLIT=0 -> the chunked instance's passes split by task
+index, else by head where that adds no wave), saved to argv[1] (.npz).
 
   get_user_vector on [64, L, 300] inputs for L = 34 (one pass over two key
   chunks), 38 (two passes split by head) and 50 (two passes, the context
