@@ -235,39 +235,47 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   // two workgroups per CU): a user whose (head, query) tasks fit the threads
   // (33, 34 titles) stages its K|V rows KVR at a time (the keys in order, each
   // chunk behind a barrier); a user with more tasks than threads (35..50
-  // titles) runs them in two passes split by HEAD (round 6): heads 0..7, then
-  // 8..14, each pass staging the K|V columns of its heads for all L keys
-  // (1,280-B rows, 64 KB at 50 keys), so every K|V byte is staged once (the
+  // titles) runs them in two passes split by HEAD (round 6): heads 0 .. hs-1,
+  // then hs .. 14, each pass staging the K|V columns of its heads for all L
+  // keys (rows of 40 hs floats), so every K|V byte is staged once (the
   // round-5 passes split by task index re-staged both key chunks in the
   // second pass: traffic 1.44x its floor) and the first pass's context is
-  // kept in registers. (At 49, 50 titles the head split leaves one more
-  // partly filled wave than the task-index split, which those users keep.) Either way each task runs the whole-tile instances'
+  // kept in registers. hs = 8, 9 or 10, the first that leaves no more partly
+  // filled waves than the task-index split (e.g. 50 titles: 10 + 5 heads, 8 + 4
+  // waves; 8 + 7 heads would be 7 + 6); none does at 46 titles, which keeps
+  // the task-index split. A 10-head tile (80,000 B at 50 keys) runs into the
+  // part / wts / rexp slots after the 76.8-KB tile, which are free until the
+  // attention's end. Either way each task runs the whole-tile instances'
   // arithmetic over the keys in the same order: bitwise their results.
-  constexpr int HS_H = 8;                      // heads of the first pass (head split)
-  constexpr int HS_W = HS_H * UDK;             // K (and V) floats of a staged row
-  constexpr int HS_RS = 2 * HS_W;              // staged row: K | V of the pass's heads
-  static_assert(!CHUNKED || (HS_H * LMAX <= NT && (UH - HS_H) * LMAX <= NT), "one pass per head group");
-  static_assert(!CHUNKED || LMAX * HS_RS <= KVR * URS, "a head group's K|V fits the tile");
+  constexpr int HS_MAX = 10;                   // most heads of the first pass
+  static_assert(!CHUNKED || (HS_MAX * LMAX <= NT && (UH - 8) * LMAX <= NT), "one pass per head group");
+  // (the last wave-instruction of a staging fills a whole 1-KB block)
+  static_assert(!CHUNKED || ((LMAX * 40 * HS_MAX / 4 + 63) / 64) * 1024 <=
+                                (KVR * URS + UNT * 64 + 64 + 2 * 64) * 4, "a head group's K|V fits the LDS");
   const int ntask = UH * L;
   const int npass = CHUNKED ? (ntask + NT - 1) / NT : 1;    // (workgroup-uniform)
-  // two passes split by head, unless that leaves more partly filled waves
-  // than the split by task index (49, 50 titles: 7 + 6 against 8 + 4 waves;
-  // same-box A/B, profiles/r6/r6c_user_head_split_ab.txt)
-  const bool hsplit = CHUNKED && npass > 1 && !(uflags & UF_TASK_SPLIT) &&
-                      (HS_H * L + 63) / 64 + ((UH - HS_H) * L + 63) / 64 <= NT / 64 + (ntask - NT + 63) / 64;
+  int hs = 0;                                               // heads of the first pass (0: no head split)
+  if (CHUNKED && npass > 1 && !(uflags & UF_TASK_SPLIT)) {
+    const int waves_task = NT / 64 + (ntask - NT + 63) / 64;
+    for (int c = HS_MAX; c >= 8; --c)
+      if (c * L <= NT && (c * L + 63) / 64 + ((UH - c) * L + 63) / 64 <= waves_task) hs = c;
+  }
+  hs = __builtin_amdgcn_readfirstlane(hs);
+  const bool hsplit = hs > 0;
+  const int hsw = UDK * hs, hrs = 2 * UDK * hs;             // K (V) floats of a staged row; its stride
   const int nchunk = CHUNKED && !hsplit ? (L + KVR - 1) / KVR : 1;
-  const int tb = hsplit ? HS_H * L : NT;                    // the second pass's first task
-  // K|V columns of heads hb .. hb + HS_H - 1 of rows 0 .. nr - 1 (head split):
-  // 80 16-B pieces per row, K's then V's; the 16th head slot of the second
-  // pass does not exist and re-reads the row's first piece (never used)
+  const int tb = hsplit ? hs * L : NT;                      // the second pass's first task
+  // K|V columns of heads hb .. hb + hs - 1 of rows 0 .. nr - 1 (head split):
+  // 10 hs 16-B pieces per row, K's then V's; head slots past 14 (the second
+  // pass) re-read the row's first piece (never used)
   auto stage_heads = [&](int hb, int nr) __attribute__((always_inline)) {
-    constexpr int PPR = HS_RS / 4, PPS = HS_W / 4;   // pieces per row / per section
-    const int np = nr * PPR;
+    const int pps = hsw / 4, ppr = 2 * pps;   // pieces per section / per row
+    const int np = nr * ppr;
     for (int p = w; p < (np + 63) >> 6; p += NT / 64) {
       int g = (p << 6) + lane;
       g = g < np ? g : np - 1;
-      const int i = g / PPR, c = g - i * PPR;
-      const int sec = c >= PPS ? 1 : 0, cc = c - sec * PPS;
+      const int i = g / ppr, c = g - i * ppr;
+      const int sec = c >= pps ? 1 : 0, cc = c - sec * pps;
       const float* src = row(i) + (1 + sec) * UD + UDK * hb + 4 * cc;
       src = hb + cc / (UDK / 4) < UH ? src : row(i) + UD;
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
@@ -288,9 +296,9 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     const bool has = task < ntask && (!hsplit || pass > 0 || tid < tb);
     const int h = has ? task / L : 0, qi = has ? task - h * L : 0;
     // head h's K and V slices within a staged row (stride krs floats)
-    const int krs = hsplit ? HS_RS : URS;
-    const int kofs = hsplit ? UDK * (h - HS_H * pass) : UDK * h;
-    const int vofs = hsplit ? HS_W + UDK * (h - HS_H * pass) : UD + UDK * h;
+    const int krs = hsplit ? hrs : URS;
+    const int kofs = hsplit ? UDK * (h - hs * pass) : UDK * h;
+    const int vofs = hsplit ? hsw + UDK * (h - hs * pass) : UD + UDK * h;
     {
       const float4* qp = reinterpret_cast<const float4*>(row(qi) + UDK * h);
 #pragma unroll
@@ -338,7 +346,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     for (int c = 0; c < nchunk; ++c) {
       const int kb = c * KVR, ke = CHUNKED && !hsplit ? (L < kb + KVR ? L : kb + KVR) : L;
       if (CHUNKED && (pass > 0 || c > 0)) __syncthreads();   // the previous chunk's readers are done
-      if (hsplit) stage_heads(HS_H * pass, L);
+      if (hsplit) stage_heads(hs * pass, L);
       else stage(kb, ke - kb);
       __syncthreads();
       if (c == 0 && pass == 0) { NRMS_U_STAMP(0) }   // K|V staged

@@ -1198,11 +1198,12 @@ def test_forward_classification_fallback_without_tail_jobs():
 
 def test_user_head_split_passes_bitwise(tmp_path):
     """The chunked UserEncoder instance (512 threads, two workgroups per CU)
-    runs users of 35..48 titles in two passes split by head, each staging its
-    heads' K|V columns for all keys once (round 6: the round-5 passes split by
-    task index staged both key chunks twice). Every (head, query) task sums
-    the same keys in the same order either way, so the user vectors (34, 38
-    and 50 rows; rows that take the recheck path included) and the bench
+    runs users of 35..50 titles (46 aside) in two passes split by head (the
+    first 8, 9 or 10 heads, then the rest), each staging its heads' K|V
+    columns for all keys once (round 6: the round-5 passes split by task
+    index staged both key chunks twice). Every (head, query) task sums the
+    same keys in the same order either way, so the user vectors (34, 36, 38,
+    41, 46 and 50 rows; rows that take the recheck path included) and the bench
     slice's logits are bitwise those of the task-index split
     (NRMS_USER_HSPLIT=0). (The 832-thread whole-tile instance pools over 8
     lanes per column instead of 4: within rounding, not bitwise.)"""
@@ -1217,7 +1218,7 @@ def test_user_head_split_passes_bitwise(tmp_path):
                             str(tmp_path / f"h{hs}.npz")], env=env, capture_output=True, text=True, timeout=300)
         assert p.returncode == 0, p.stderr[-3000:]
         outs[hs] = np.load(tmp_path / f"h{hs}.npz")
-    for k in ("uv34", "uv38", "uv50", "logits"):
+    for k in ("uv34", "uv36", "uv38", "uv41", "uv46", "uv50", "logits"):
         a, b = outs["0"][k], outs["1"][k]
         assert np.isfinite(b).any()
         assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k

@@ -4,8 +4,8 @@ the form: NRMS_USER_HSPLIT=0 -> the chunked instance's passes split by task
 index, else by head where that adds no wave), saved to argv[1] (.npz).
 
   get_user_vector on [64, L, 300] inputs for L = 34 (one pass over two key
-  chunks), 38 (two passes split by head) and 50 (two passes, the context
-  packed as two planes), scaled so some rows take the recheck path, and
+  chunks), 36 / 41 / 38, 50 (two passes split 8 + 7 / 9 + 6 / 10 + 5 heads),
+  46 (split by task index; past 39 rows the context packed as two planes), scaled so some rows take the recheck path, and
   nrms_forward logits on a 256-impression slice of the bench batch
   (compacted lengths 1..50)."""
 import os
@@ -26,7 +26,7 @@ def main(out):
     model = bench.build_model(dev)
     res = {}
     with torch.no_grad():
-        for L in (34, 38, 50):
+        for L in (34, 36, 38, 41, 46, 50):
             g = torch.Generator(device="cpu").manual_seed(4 + L)
             x = torch.randn(64, L, 300, generator=g)
             x[::7] *= 30.0                      # large scores: rows near fp32 overflow take the recheck path
