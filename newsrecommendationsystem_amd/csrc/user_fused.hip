@@ -247,7 +247,10 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   // part / wts / rexp slots after the 76.8-KB tile, which are free until the
   // attention's end. Either way each task runs the whole-tile instances'
   // arithmetic over the keys in the same order: bitwise their results.
-  constexpr int HS_MAX = 10;                   // most heads of the first pass
+#ifndef NRMS_USER_HS_MAX
+#define NRMS_USER_HS_MAX 10
+#endif
+  constexpr int HS_MAX = NRMS_USER_HS_MAX;     // most heads of the first pass
   static_assert(!CHUNKED || (HS_MAX * LMAX <= NT && (UH - 8) * LMAX <= NT), "one pass per head group");
   // (the last wave-instruction of a staging fills a whole 1-KB block)
   static_assert(!CHUNKED || ((LMAX * 40 * HS_MAX / 4 + 63) / 64) * 1024 <=
@@ -258,18 +261,19 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   if (CHUNKED && npass > 1 && !(uflags & UF_TASK_SPLIT)) {
     const int waves_task = NT / 64 + (ntask - NT + 63) / 64;
     for (int c = HS_MAX; c >= 8; --c)
+#ifdef NRMS_USER_HS_SKIP9
+      if (c != 9)
+#endif
       if (c * L <= NT && (c * L + 63) / 64 + ((UH - c) * L + 63) / 64 <= waves_task) hs = c;
   }
   hs = __builtin_amdgcn_readfirstlane(hs);
   const bool hsplit = hs > 0;
-  const int hsw = UDK * hs, hrs = 2 * UDK * hs;             // K (V) floats of a staged row; its stride
   const int nchunk = CHUNKED && !hsplit ? (L + KVR - 1) / KVR : 1;
   const int tb = hsplit ? hs * L : NT;                      // the second pass's first task
-  // K|V columns of heads hb .. hb + hs - 1 of rows 0 .. nr - 1 (head split):
-  // 10 hs 16-B pieces per row, K's then V's; head slots past 14 (the second
-  // pass) re-read the row's first piece (never used)
-  auto stage_heads = [&](int hb, int nr) __attribute__((always_inline)) {
-    const int pps = hsw / 4, ppr = 2 * pps;   // pieces per section / per row
+  // K|V columns of heads hb .. hb + nh - 1 of rows 0 .. nr - 1 (head split):
+  // 10 nh 16-B pieces per row (stride 40 nh floats), K's then V's
+  auto stage_heads = [&](int hb, int nh, int nr) __attribute__((always_inline)) {
+    const int pps = nh * (UDK / 4), ppr = 2 * pps;   // pieces per section / per row
     const int np = nr * ppr;
     for (int p = w; p < (np + 63) >> 6; p += NT / 64) {
       int g = (p << 6) + lane;
@@ -277,7 +281,6 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       const int i = g / ppr, c = g - i * ppr;
       const int sec = c >= pps ? 1 : 0, cc = c - sec * pps;
       const float* src = row(i) + (1 + sec) * UD + UDK * hb + 4 * cc;
-      src = hb + cc / (UDK / 4) < UH ? src : row(i) + UD;
       __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
                                        (__attribute__((address_space(3))) void*)(tile + (p << 8)), 16, 0, 0);
     }
@@ -296,9 +299,11 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     const bool has = task < ntask && (!hsplit || pass > 0 || tid < tb);
     const int h = has ? task / L : 0, qi = has ? task - h * L : 0;
     // head h's K and V slices within a staged row (stride krs floats)
-    const int krs = hsplit ? hrs : URS;
-    const int kofs = hsplit ? UDK * (h - hs * pass) : UDK * h;
-    const int vofs = hsplit ? hsw + UDK * (h - hs * pass) : UD + UDK * h;
+    // (head split: this pass's heads h0 .. h0 + nh - 1, rows of 40 nh floats)
+    const int h0 = hs * pass, nh = pass == 0 ? hs : UH - hs;
+    const int krs = hsplit ? 2 * UDK * nh : URS;
+    const int kofs = hsplit ? UDK * (h - h0) : UDK * h;
+    const int vofs = hsplit ? UDK * nh + UDK * (h - h0) : UD + UDK * h;
     {
       const float4* qp = reinterpret_cast<const float4*>(row(qi) + UDK * h);
 #pragma unroll
@@ -346,7 +351,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     for (int c = 0; c < nchunk; ++c) {
       const int kb = c * KVR, ke = CHUNKED && !hsplit ? (L < kb + KVR ? L : kb + KVR) : L;
       if (CHUNKED && (pass > 0 || c > 0)) __syncthreads();   // the previous chunk's readers are done
-      if (hsplit) stage_heads(hs * pass, L);
+      if (hsplit) stage_heads(h0, nh, L);
       else stage(kb, ke - kb);
       __syncthreads();
       if (c == 0 && pass == 0) { NRMS_U_STAMP(0) }   // K|V staged
