@@ -101,6 +101,10 @@ constexpr int UF_COPIED = 1, UF_COMPACT = 2;
 // round-5 form) even where the head split adds no wave (NRMS_USER_HSPLIT=0:
 // the test that the head split changes no bit)
 constexpr int UF_TASK_SPLIT = 4;
+// UF_NO_PAIR: the chunked instance's long users (more tasks than threads) in
+// two passes (split by head or task index) instead of two queries per thread
+// in one pass (NRMS_USER_PAIR=0: the test that the pairing changes no bit)
+constexpr int UF_NO_PAIR = 8;
 #ifndef NRMS_USER_WDEPTH
 #define NRMS_USER_WDEPTH 4
 #endif
@@ -140,7 +144,10 @@ __global__ __launch_bounds__(UORD_T) void user_order_kernel(const uint8_t* __res
 }
 
 template <int MODE, int LMAX, int NT, int KVR = LMAX>
-__global__ __launch_bounds__(NT, 1) void fused_user_kernel(
+#ifndef NRMS_USER_CHUNK_MINWAVES
+#define NRMS_USER_CHUNK_MINWAVES 4
+#endif
+__global__ __launch_bounds__(NT, (KVR < LMAX) ? NRMS_USER_CHUNK_MINWAVES : 1) void fused_user_kernel(
     const float* __restrict__ qkv, int64_t ldq, int L_all, const float* __restrict__ WaP,
     const float* __restrict__ b_add, const float* __restrict__ q_add, float* __restrict__ out,
     PaddingGroups pg, int uflags, const int32_t* __restrict__ order, ScoreFold sf) {
@@ -257,8 +264,18 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
                                 (KVR * URS + UNT * 64 + 64 + 2 * 64) * 4, "a head group's K|V fits the LDS");
   const int ntask = UH * L;
   const int npass = CHUNKED ? (ntask + NT - 1) / NT : 1;    // (workgroup-uniform)
+  // two queries of one head per thread, one pass over two key chunks (round
+  // 6, see the attention below): 15 ceil(L / 2) <= 375 tasks
+#ifndef NRMS_USER_PAIR_MIN
+#define NRMS_USER_PAIR_MIN 35
+#endif
+#ifndef NRMS_USER_NO_PAIR_CODE
+  const bool pairmode = CHUNKED && (npass > 1 || L >= NRMS_USER_PAIR_MIN) && !(uflags & UF_NO_PAIR);
+#else
+  const bool pairmode = false;   // (probe builds without the paired path)
+#endif
   int hs = 0;                                               // heads of the first pass (0: no head split)
-  if (CHUNKED && npass > 1 && !(uflags & UF_TASK_SPLIT)) {
+  if (CHUNKED && npass > 1 && !pairmode && !(uflags & UF_TASK_SPLIT)) {
     const int waves_task = NT / 64 + (ntask - NT + 63) / 64;
     for (int c = HS_MAX; c >= 8; --c)
 #ifdef NRMS_USER_HS_SKIP9
@@ -269,6 +286,7 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   hs = __builtin_amdgcn_readfirstlane(hs);
   const bool hsplit = hs > 0;
   const int nchunk = CHUNKED && !hsplit ? (L + KVR - 1) / KVR : 1;
+  const int npair = (L + 1) / 2;                            // (pairmode) query pairs per head
   const int tb = hsplit ? hs * L : NT;                      // the second pass's first task
   // K|V columns of heads hb .. hb + nh - 1 of rows 0 .. nr - 1 (head split):
   // 10 nh 16-B pieces per row (stride 40 nh floats), K's then V's
@@ -294,7 +312,158 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
   float acc[UDK], q[UDK];
   [[maybe_unused]] float acc0[UDK];   // CHUNKED, two passes: the first pass's context
   float mrow = 0.f, mrow0 = 0.f;      // MODE 2: max |ctx| of this thread's task (per pass)
-  for (int pass = 0; pass < npass; ++pass) {
+  // ---- pairmode (CHUNKED, 35..50 rows): thread = (head h, queries 2p, 2p + 1)
+  // The attention of the long users was bound by the LDS returns of its
+  // broadcast K|V reads (160 B per key per (head, query) task at 256 B/clk/CU
+  // against ~half that time of VALU work); with two queries per thread each
+  // K|V slice read serves both, so the bytes halve, the 15 ceil(L / 2) <= 375
+  // tasks fit one pass and the keys are staged once, in two chunks. Each
+  // query runs exactly the single-query arithmetic (the same dot product,
+  // exp, key order of the sums, four-key groups with weight-0 padding, and
+  // recheck path): bitwise the two-pass forms' results.
+  [[maybe_unused]] float q1[UDK];
+  [[maybe_unused]] float mrow1 = 0.f;
+  [[maybe_unused]] const bool phas = pairmode && tid < UH * npair;
+  [[maybe_unused]] const int ph = phas ? tid / npair : 0, pq = phas ? 2 * (tid - ph * npair) : 0;
+  [[maybe_unused]] const bool phas1 = phas && pq + 1 < L;
+  if constexpr (CHUNKED) {
+#ifndef NRMS_USER_NO_PAIR_CODE
+    if (pairmode) {
+      auto loadq = [&](float (&qq)[UDK], int qi) __attribute__((always_inline)) {
+        const float4* qp = reinterpret_cast<const float4*>(row(qi) + UDK * ph);
+#pragma unroll
+        for (int t = 0; t < UDK / 4; ++t) {
+          const float4 v = qp[t];
+          qq[4 * t] = v.x; qq[4 * t + 1] = v.y; qq[4 * t + 2] = v.z; qq[4 * t + 3] = v.w;
+        }
+      };
+      loadq(q, pq);
+      loadq(q1, phas1 ? pq + 1 : pq);
+      // both queries' dot products with one K slice read (the single-query
+      // form's even / odd partial sums), and both context updates with one V
+      auto dot2 = [&](const float* kp, float& da, float& db) __attribute__((always_inline)) {
+        const float4* kr = reinterpret_cast<const float4*>(kp);
+        f2 a = f2{0.f, 0.f}, b = f2{0.f, 0.f};
+#pragma unroll
+        for (int t = 0; t < UDK / 4; ++t) {
+          const float4 k4 = kr[t];
+          a = __builtin_elementwise_fma(f2{q[4 * t], q[4 * t + 1]}, f2{k4.x, k4.y}, a);
+          a = __builtin_elementwise_fma(f2{q[4 * t + 2], q[4 * t + 3]}, f2{k4.z, k4.w}, a);
+          b = __builtin_elementwise_fma(f2{q1[4 * t], q1[4 * t + 1]}, f2{k4.x, k4.y}, b);
+          b = __builtin_elementwise_fma(f2{q1[4 * t + 2], q1[4 * t + 3]}, f2{k4.z, k4.w}, b);
+        }
+        da = a.x + a.y;
+        db = b.x + b.y;
+      };
+      auto axpy2 = [&](float ea, float eb, const float* vp) __attribute__((always_inline)) {
+        const float4* vr = reinterpret_cast<const float4*>(vp);
+        const f2 a2 = f2{ea, ea}, b2 = f2{eb, eb};
+#pragma unroll
+        for (int t = 0; t < UDK / 4; ++t) {
+          const float4 v4 = vr[t];
+          const f2 lo = __builtin_elementwise_fma(a2, f2{v4.x, v4.y}, f2{acc[4 * t], acc[4 * t + 1]});
+          const f2 hi = __builtin_elementwise_fma(a2, f2{v4.z, v4.w}, f2{acc[4 * t + 2], acc[4 * t + 3]});
+          acc[4 * t] = lo.x; acc[4 * t + 1] = lo.y; acc[4 * t + 2] = hi.x; acc[4 * t + 3] = hi.y;
+          const f2 lo1 = __builtin_elementwise_fma(b2, f2{v4.x, v4.y}, f2{acc0[4 * t], acc0[4 * t + 1]});
+          const f2 hi1 = __builtin_elementwise_fma(b2, f2{v4.z, v4.w}, f2{acc0[4 * t + 2], acc0[4 * t + 3]});
+          acc0[4 * t] = lo1.x; acc0[4 * t + 1] = lo1.y; acc0[4 * t + 2] = hi1.x; acc0[4 * t + 3] = hi1.y;
+        }
+      };
+#pragma unroll
+      for (int t = 0; t < UDK; ++t) { acc[t] = 0.f; acc0[t] = 0.f; }
+      float sa = 0.f, sb = 0.f;
+      for (int c = 0; c < nchunk; ++c) {
+        const int kb = c * KVR, ke = L < kb + KVR ? L : kb + KVR;
+        if (c > 0) __syncthreads();   // the previous chunk's readers are done
+        stage(kb, ke - kb);
+        __syncthreads();
+        if (c == 0) { NRMS_U_STAMP(0) }   // K|V staged
+        if (phas) {
+          const float* kt = tile - (int64_t)kb * URS + UDK * ph;   // key j's K slice: kt + j URS
+          // one key per iteration, rolled (the four-key unrolled form of the
+          // single-query loop, with weight-0 padding keys: 56 KB of code, 128
+          // VGPRs + scratch, user_fused 0.0700 against 0.0676 ms,
+          // profiles/r6/r6l_user_pair_ab.txt). Without the padding keys the
+          // sums and context updates are the same operations on the same
+          // values: a padding key adds 0 to the sum and 0·v to a context that
+          // starts at +0 (never -0), and a non-finite v makes the real key's
+          // update non-finite too (recheck path) -- bitwise the padded forms.
+#pragma unroll 1
+          for (int j = kb; j < ke; ++j) {
+            float da, db;
+            dot2(kt + j * URS, da, db);
+            float ea = __builtin_amdgcn_exp2f(da * rs), eb = __builtin_amdgcn_exp2f(db * rs);
+            if (j == 0) {
+              for (int cc = 0; cc < m0; ++cc) { sa += ea; sb += eb; }   // (row 0's multiplicity)
+              ea *= (float)m0;
+              eb *= (float)m0;
+            } else {
+              sa += ea;
+              sb += eb;
+            }
+            axpy2(ea, eb, kt + j * URS + UD);
+          }
+        }
+      }
+      if (phas) {
+        // normalisation, or (rare) the reference-order recheck, per query
+        auto finish = [&](const float (&qq)[UDK], float (&aa)[UDK], float sum) __attribute__((always_inline)) {
+          bool finite = true;
+#pragma unroll
+          for (int t = 0; t < UDK; ++t) finite &= __builtin_isfinite(aa[t]);
+          if (!exp_row_needs_recheck(sum) && finite) {
+            const float inv = 1.0f / (sum + 1e-8f);
+#pragma unroll
+            for (int t = 0; t < UDK; ++t) aa[t] *= inv;
+          } else {
+            auto dotq = [&](const float* kp) __attribute__((always_inline)) {
+              const float4* kr = reinterpret_cast<const float4*>(kp);
+              f2 d = f2{0.f, 0.f};
+#pragma unroll
+              for (int t = 0; t < UDK / 4; ++t) {
+                const float4 k4 = kr[t];
+                d = __builtin_elementwise_fma(f2{qq[4 * t], qq[4 * t + 1]}, f2{k4.x, k4.y}, d);
+                d = __builtin_elementwise_fma(f2{qq[4 * t + 2], qq[4 * t + 3]}, f2{k4.z, k4.w}, d);
+              }
+              return d.x + d.y;
+            };
+            float s2 = 0.f;
+            for (int j = 0; j < L; ++j) {
+              const float x = ref_exp(dotq(row(j) + UD + UDK * ph), sqrt_dk);
+              if (j == 0)
+                for (int cc = 0; cc < m0; ++cc) s2 += x;
+              else
+                s2 += x;
+            }
+            const float inv = 1.0f / (s2 + 1e-8f);
+#pragma unroll
+            for (int t = 0; t < UDK; ++t) aa[t] = 0.f;
+            for (int j = 0; j < L; ++j) {
+              float a = ref_exp(dotq(row(j) + UD + UDK * ph), sqrt_dk) * inv;
+              if (j == 0 && m0 > 1) a *= (float)m0;
+              const float4* vr = reinterpret_cast<const float4*>(row(j) + 2 * UD + UDK * ph);
+              const f2 a2 = f2{a, a};
+#pragma unroll
+              for (int t = 0; t < UDK / 4; ++t) {
+                const float4 v4 = vr[t];
+                const f2 lo = __builtin_elementwise_fma(a2, f2{v4.x, v4.y}, f2{aa[4 * t], aa[4 * t + 1]});
+                const f2 hi = __builtin_elementwise_fma(a2, f2{v4.z, v4.w}, f2{aa[4 * t + 2], aa[4 * t + 3]});
+                aa[4 * t] = lo.x; aa[4 * t + 1] = lo.y; aa[4 * t + 2] = hi.x; aa[4 * t + 3] = hi.y;
+              }
+            }
+          }
+          float m = 0.f;
+#pragma unroll
+          for (int t = 0; t < UDK; ++t) m = fmaxf(m, fabsf(aa[t]));
+          return m;
+        };
+        mrow = finish(q, acc, sa);
+        mrow1 = finish(q1, acc0, sb);
+      }
+    }
+#endif
+  }
+  for (int pass = 0; pass < (pairmode ? 0 : npass); ++pass) {
     const int task = tb * pass + tid;
     const bool has = task < ntask && (!hsplit || pass > 0 || tid < tb);
     const int h = has ? task / L : 0, qi = has ? task - h * L : 0;
@@ -448,8 +617,13 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
     [[maybe_unused]] const bool has0 = hsplit ? tid < tb : tid < ntask;
     [[maybe_unused]] const bool has1 = npass > 1 && tb + tid < ntask;
     if constexpr (CHUNKED) {
-      if (has0) part[tid] = npass > 1 ? mrow0 : mrow;
-      if (has1) part[tb + tid] = mrow;
+      if (pairmode) {
+        if (phas) part[ph * L + pq] = mrow;
+        if (phas1) part[ph * L + pq + 1] = mrow1;
+      } else {
+        if (has0) part[tid] = npass > 1 ? mrow0 : mrow;
+        if (has1) part[tb + tid] = mrow;
+      }
       __syncthreads();
     }
     // three fp16 planes per row (hi | lo | r), in the MODE 1 positions
@@ -478,7 +652,10 @@ __global__ __launch_bounds__(NT, 1) void fused_user_kernel(
       }
     };
     if constexpr (CHUNKED) {
-      if (npass > 1) {
+      if (pairmode) {
+        if (phas) write_ctx(ph * L + pq, acc);
+        if (phas1) write_ctx(ph * L + pq + 1, acc0);
+      } else if (npass > 1) {
         if (has0) write_ctx(tid, acc0);
         if (has1) write_ctx(tb + tid, acc);
       } else if (has) {
@@ -859,6 +1036,11 @@ int32_t launch_user_mode(const float* qkv, int64_t ldq, int64_t B, int L, const 
 
 size_t fused_user_packed_b_floats() { return (size_t)UWAP_MAX + USTAMP_FLOATS; }
 
+static std::atomic<int> g_user_pair{[] {
+  const char* e = env_knob("NRMS_USER_PAIR");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
+
 static std::atomic<int> g_user_hsplit{[] {
   const char* e = env_knob("NRMS_USER_HSPLIT");
   return (e && e[0] == '0') ? 0 : 1;
@@ -882,7 +1064,8 @@ int32_t launch_fused_user(const float* qkv, int64_t ldq, int64_t B, int L, const
   if (compact && (!pgp || L > 64 || B * L > INT32_MAX)) return NRMS_ERR_UNSUPPORTED;
   if (copied && !pgp) return NRMS_ERR_INVALID_ARG;
   const int uflags = (copied ? UF_COPIED : 0) | (compact ? UF_COMPACT : 0) |
-                     (g_user_hsplit.load(std::memory_order_relaxed) ? 0 : UF_TASK_SPLIT);
+                     (g_user_hsplit.load(std::memory_order_relaxed) ? 0 : UF_TASK_SPLIT) |
+                     (g_user_pair.load(std::memory_order_relaxed) ? 0 : UF_NO_PAIR);
   if (B == 0) return NRMS_OK;
   if (!fused_user_supported(L, UD, UH, UQ) || B > INT32_MAX) return NRMS_ERR_UNSUPPORTED;
   if (((uintptr_t)qkv | (uintptr_t)out | (uintptr_t)wap) % 16 || ldq < 3 * UD || ldq % 4)

@@ -1196,29 +1196,32 @@ def test_forward_classification_fallback_without_tail_jobs():
 
 
 
-def test_user_head_split_passes_bitwise(tmp_path):
+def test_user_long_history_forms_bitwise(tmp_path):
     """The chunked UserEncoder instance (512 threads, two workgroups per CU)
-    runs users of 35..50 titles (46 aside) in two passes split by head (the
-    first 8, 9 or 10 heads, then the rest), each staging its heads' K|V
-    columns for all keys once (round 6: the round-5 passes split by task
-    index staged both key chunks twice). Every (head, query) task sums the
-    same keys in the same order either way, so the user vectors (34, 36, 38,
-    41, 46 and 50 rows; rows that take the recheck path included) and the bench
-    slice's logits are bitwise those of the task-index split
-    (NRMS_USER_HSPLIT=0). (The 832-thread whole-tile instance pools over 8
-    lanes per column instead of 4: within rounding, not bitwise.)"""
+    has three forms for a user with more (head, query) tasks than threads
+    (35..50 titles), all running the single-query arithmetic over the keys in
+    the same order: two queries of one head per thread in one pass over two
+    key chunks (round 6, the default), two passes split by head (the first 8,
+    9 or 10 heads, then the rest; NRMS_USER_PAIR=0), and the round-5 two
+    passes split by task index (NRMS_USER_PAIR=0 NRMS_USER_HSPLIT=0). The
+    user vectors at 34, 36, 38, 41, 46 and 50 rows (rows that take the
+    recheck path included) and a 256-impression bench slice's logits are
+    bitwise equal across the three. (The 832-thread whole-tile instance pools
+    over 8 lanes per column instead of 4: within rounding, not bitwise.)"""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
-    for hs in ("0", "1"):
-        env = dict(os.environ, NRMS_USER_HSPLIT=hs)
+    for tag, env_add in (("pair", {}), ("heads", {"NRMS_USER_PAIR": "0"}),
+                         ("tasks", {"NRMS_USER_PAIR": "0", "NRMS_USER_HSPLIT": "0"})):
+        env = dict(os.environ, **env_add)
         p = subprocess.run([sys.executable, os.path.join(root, "tests", "user_chunk_worker.py"),
-                            str(tmp_path / f"h{hs}.npz")], env=env, capture_output=True, text=True, timeout=300)
+                            str(tmp_path / f"{tag}.npz")], env=env, capture_output=True, text=True, timeout=300)
         assert p.returncode == 0, p.stderr[-3000:]
-        outs[hs] = np.load(tmp_path / f"h{hs}.npz")
+        outs[tag] = np.load(tmp_path / f"{tag}.npz")
     for k in ("uv34", "uv36", "uv38", "uv41", "uv46", "uv50", "logits"):
-        a, b = outs["0"][k], outs["1"][k]
-        assert np.isfinite(b).any()
-        assert np.array_equal(a.view(np.uint32), b.view(np.uint32)), k
+        a = outs["tasks"][k]
+        assert np.isfinite(a).any()
+        for tag in ("pair", "heads"):
+            assert np.array_equal(outs[tag][k].view(np.uint32), a.view(np.uint32)), (tag, k)

@@ -1,7 +1,9 @@
-"""Child process of tests/test_gpu_parity.py::test_user_head_split_passes_bitwise:
+"""Child process of tests/test_gpu_parity.py::test_user_long_history_forms_bitwise:
 the UserEncoder outputs of one library configuration (the environment picks
-the form: NRMS_USER_HSPLIT=0 -> the chunked instance's passes split by task
-index, else by head where that adds no wave), saved to argv[1] (.npz).
+the chunked instance's form for long users: two queries per thread in one
+pass by default; NRMS_USER_PAIR=0 -> two passes split by head where that
+adds no wave; + NRMS_USER_HSPLIT=0 -> two passes split by task index), saved
+to argv[1] (.npz).
 
   get_user_vector on [64, L, 300] inputs for L = 34 (one pass over two key
   chunks), 36 / 41 / 38, 50 (two passes split 8 + 7 / 9 + 6 / 10 + 5 heads),
