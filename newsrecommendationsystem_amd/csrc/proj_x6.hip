@@ -23,7 +23,7 @@
 // the two kernels agree bitwise (tests/test_gpu_parity.py compares them).
 //
 // H3 (the default arithmetic, NRMS_GEMM_SPLIT_F16X3): split-f16 with
-// power-of-two scaling, four products instead of six. Every A row and every
+// power-of-two scaling, three or four products instead of six. Every A row and every
 // W row (output column) is scaled by its own power of two, 2^-ea (row max
 // into [2^3, 2^4)) and 2^-ew (into [2^14, 2^15)), which is exact and puts both
 // in fp16's range whatever their magnitude. A is split into three fp16
@@ -37,8 +37,13 @@
 // fp32 GEMM rounding (tests bound them against an fp64 oracle), and a W that
 // fits in 11 bits (e.g. the overflow-boundary fixtures' one-hot W_Q) gives
 // products as exact as fp32's — the reference's raw-exp overflow boundary is
-// reproduced. W streams as two fp16 planes instead of three bf16 planes. A
-// NaN stays NaN; an infinite input gives NaN in its row (column), as x6.
+// reproduced. That exactness is all the fourth product, w_hi·r (A's bits past
+// 22), adds: where a column's w_lo is non-zero, the dropped w_lo·(lo + r) is
+// of its size. So the kernel runs three products (w_lo·a_hi, w_hi·a_lo,
+// w_hi·(2^11 a_hi); no r plane staged) unless some column of the weight set
+// fits in 11 bits (the pack's column flags; NRMS_PROJ_PRODUCTS=4 forces four).
+// W streams as two fp16 planes instead of three bf16 planes. A NaN stays NaN;
+// an infinite input gives NaN in its row (column), as x6.
 
 #include "nrms_common.hpp"
 #include "packs.hpp"
@@ -74,9 +79,11 @@ constexpr int PSTAMP_FLOATS = 256 * 8 * 8 * 2;
 #else
 constexpr int PSTAMP_FLOATS = 0;
 #endif
-// [fragments (x6: 3 bf16 planes, H3: 2 fp16 planes)][bias][zero row][NaN row][trash][H3 column exponents][stamps]
+// [fragments (x6: 3 bf16 planes, H3: 2 fp16 planes)][bias][zero row][NaN row][trash][H3 column exponents]
+// [H3 column flags: 1 = no fourth product (W has bits past 11, or the column is past N)][stamps]
 constexpr int OFF_BIAS = PACK_BF16 / 2, OFF_ZERO = OFF_BIAS + PNT * 16, OFF_NAN = OFF_ZERO + PKP;
-constexpr int OFF_TRASH = OFF_NAN + PKP, OFF_EXP = OFF_TRASH + PTRASH, OFF_STAMP = OFF_EXP + PNT * 16;
+constexpr int OFF_TRASH = OFF_NAN + PKP, OFF_EXP = OFF_TRASH + PTRASH, OFF_WRES = OFF_EXP + PNT * 16;
+constexpr int OFF_STAMP = OFF_WRES + PNT * 16;
 constexpr int PACK_FLOATS = OFF_STAMP + PSTAMP_FLOATS;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -131,8 +138,10 @@ __device__ __forceinline__ void pack_proj(int idx, const WeightRows& w, float* _
 // H3: one wave per W row n < 16 PNT (rows past N: zeros), lane k = lane + 64 i
 // (i < 5 covers the K padding to 320): the row's max |w| (wave reduction)
 // gives its exponent ew; [ks][nt][plane hi | lo][lane][8 f16] as the x6
-// fragments; lane 0 writes the bias and ew. Block PACK_ROWS_H3 / 4 writes the
-// zero and NaN rows.
+// fragments; lane 0 writes the bias, ew and whether the column can do
+// without the projection's fourth product (an element of the row has bits
+// past hi, so lo != 0; columns past N: yes). Block
+// PACK_ROWS_H3 / 4 writes the zero and NaN rows.
 constexpr int PACK_BLOCKS_H3 = PNT * 16 / 4 + 1;
 __device__ __forceinline__ void pack_proj_h3(int b, int t, const WeightRows& w, float* __restrict__ dst) {
   if (b == PACK_BLOCKS_H3 - 1) {
@@ -143,6 +152,7 @@ __device__ __forceinline__ void pack_proj_h3(int b, int t, const WeightRows& w, 
   const int seg = n < PN ? n / w.seg_rows : 0;
   const float* wr = w.w[seg] + (int64_t)(n - seg * w.seg_rows) * PK;
   float v[5], mx = 0.f;
+  bool inexact = false;
 #pragma unroll
   for (int i = 0; i < 5; ++i) {
     const int k = lane + 64 * i;
@@ -159,14 +169,18 @@ __device__ __forceinline__ void pack_proj_h3(int b, int t, const WeightRows& w, 
     const int k = lane + 64 * i, ks = k >> 5, kq = (k >> 3) & 3;
     const float x = ldexpf(v[i], -ew);
     const _Float16 hi = (_Float16)x;
-    const _Float16 lo = (_Float16)((x - (float)hi) * kTwo11);
+    const float r1 = (x - (float)hi) * kTwo11;   // exact
+    const _Float16 lo = (_Float16)r1;
+    inexact |= !(x == (float)hi);                 // bits past 11 (NaN: inexact)
     const int e = ((ks * PNT + nt) * 2) * 512 + (r + 16 * kq) * 8 + (k & 7);
     o[e] = hi;
     o[e + 512] = lo;
   }
+  const bool row_inexact = __ballot(inexact) != 0;
   if (lane == 0) {
     dst[OFF_BIAS + n] = (n < PN && w.b[seg]) ? w.b[seg][n - seg * w.seg_rows] : 0.f;
     reinterpret_cast<int32_t*>(dst)[OFF_EXP + n] = ew;
+    reinterpret_cast<int32_t*>(dst)[OFF_WRES + n] = (row_inexact || n >= PN) ? 1 : 0;
   }
 }
 
@@ -232,7 +246,7 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
                                                             const int64_t* __restrict__ row_ids, int64_t M,
                                                             const float* __restrict__ packed, float* __restrict__ Y,
                                                             int64_t ldy, const int32_t* __restrict__ m_dev,
-                                                            tl::TailJobs tj) {
+                                                            tl::TailJobs tj, int force4) {
   static_assert(NW == 4 || NW == 8, "waves per workgroup");
   constexpr int NTH = 64 * NW;
   constexpr int TPR = NTH / PM;                      // threads per A row (4 or 8)
@@ -330,6 +344,14 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
 #endif
     }
   };
+  // H3 on three products unless some W column fits in 11 bits (the pack's
+  // column flags, read by every workgroup; header comment).
+  bool p4 = true;
+  int p3_cols = 1;
+  if constexpr (H3) {
+    const int32_t* wres0 = reinterpret_cast<const int32_t*>(packed) + OFF_WRES;
+    for (int c = threadIdx.x; c < PNT * 16; c += NTH) p3_cols &= wres0[c];
+  }
   auto store_a = [&](int64_t o) __attribute__((always_inline)) {
     if constexpr (H3) {
       // the row's max |a| over its TPR threads (consecutive lanes; pieces past
@@ -359,7 +381,7 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
           typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
           *reinterpret_cast<f16x4*>(d) = f16x4{h[0], h[1], h[2], h[3]};
           *reinterpret_cast<f16x4*>(d + PKP) = f16x4{l[0], l[1], l[2], l[3]};
-          *reinterpret_cast<f16x4*>(d + 2 * PKP) = f16x4{r[0], r[1], r[2], r[3]};
+          if (p4) *reinterpret_cast<f16x4*>(d + 2 * PKP) = f16x4{r[0], r[1], r[2], r[3]};
         }
       }
       if (aq == 0) {
@@ -390,6 +412,7 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
     // the tail jobs (titles.hpp) under the first A tile's loads: after the
     // last item they added their dependent loads to the kernel's end
     if (tail) tl::run_tail_jobs<NTH>(tj, tid);
+    if constexpr (H3) p4 = force4 || !__syncthreads_and(p3_cols);
     store_a(a0.o);
   }
   __syncthreads();
@@ -419,7 +442,8 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
   // copy and not stored — those waves would otherwise wait at the next restage
   // barrier for the waves with live tiles.
   const int off_w = NW == 4 ? PTW * w : (w < 4 ? 3 * w : 12 + 2 * (w - 4));
-  auto run = [&](auto cc) __attribute__((always_inline)) {
+  // p4c: H3 on four products, or three (below)
+  auto run = [&](auto cc, auto p4c) __attribute__((always_inline)) {
     constexpr int C = decltype(cc)::value;
     auto tile_of = [&](int64_t item, int j) __attribute__((always_inline)) -> int {
       const int t = (int)(item % PNR) * PRANGE + off_w + j;
@@ -439,9 +463,10 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
     };
     // A fragments of one k-step in the order the products use them (x6: lo
     // planes first; H3: hi, lo, hi')
-    auto load_afrag = [&](int ks, frag (&a)[PMT][3]) __attribute__((always_inline)) {
+    auto load_afrag = [&](int ks, frag (&a)[PMT][3], auto p4c) __attribute__((always_inline)) {
+      constexpr int NAP = (H3 && !decltype(p4c)::value) ? 2 : 3;   // A planes read
 #pragma unroll
-      for (int q = 0; q < 3; ++q) {
+      for (int q = 0; q < NAP; ++q) {
         const int pl = H3 ? q : 2 - q;
 #pragma unroll
         for (int mt = 0; mt < PMT; ++mt)
@@ -467,10 +492,10 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
 #pragma unroll
       for (int mt = 0; mt < PMT; ++mt) hs[mt] = a[mt][0] * (_Float16)kTwo11;
     };
-    auto kstep = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL]) __attribute__((always_inline)) {
+    auto kstep = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL], auto p4c) __attribute__((always_inline)) {
       if constexpr (H3) {
 #pragma unroll
-        for (int p = 0; p < 3; ++p)
+        for (int p = decltype(p4c)::value ? 0 : 1; p < 3; ++p)
 #pragma unroll
           for (int j = 0; j < C; ++j)
 #pragma unroll
@@ -580,14 +605,15 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
       // the last k-step tile by tile, each tile's stores issued behind the next
       // tile's MFMAs (the store bursts of all CUs at an item's end cost ~17 % of
       // the kernel; here they run under the MFMAs)
-      auto kstep_final = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL]) __attribute__((always_inline)) {
+      auto kstep_final = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL], auto p4c)
+          __attribute__((always_inline)) {
         [[maybe_unused]] frag hs[PMT];
         if constexpr (H3) hi_scaled(a, hs);
 #pragma unroll
         for (int j = 0; j < C; ++j) {
           if constexpr (H3) {
 #pragma unroll
-            for (int p = 0; p < 4; ++p)
+            for (int p = decltype(p4c)::value ? 0 : 1; p < 4; ++p)
 #pragma unroll
               for (int mt = 0; mt < PMT; ++mt)
                 mfma_h(bb[j][p == 1 ? 1 : 0], p == 3 ? hs[mt] : a[mt][p == 0 ? 2 : p == 1 ? 0 : 1], mt, j);
@@ -604,36 +630,38 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
         store_tile(C - 1);
       };
       constexpr bool A2 = NW == 4;
-      frag a0[PMT][3], a1[PMT][3];
-      if constexpr (A2) load_afrag(0, a0);
+      {
+        frag a0[PMT][3], a1[PMT][3];
+        if constexpr (A2) load_afrag(0, a0, p4c);
 #pragma unroll
-      for (int ks = 0; ks < PKS; ks += 2) {
-        load_b(ks + 1, bvoff, b1);
-        if constexpr (A2) load_afrag(ks + 1, a1);
-        else load_afrag(ks, a0);
-        __builtin_amdgcn_sched_barrier(0);
-        kstep(a0, b0);
-        __builtin_amdgcn_sched_barrier(0);
-        if (ks == 0) { NRMS_PX_STAMP(1) }   // item setup + first k-step (B(0) / A fragment waits)
-        if (ks + 2 < PKS) {
-          load_b(ks + 2, bvoff, b0);
-          if constexpr (A2) load_afrag(ks + 2, a0);
-        } else {
-          // unconditional (the last item reloads its own first k-step): behind a
-          // branch, the waitcnt pass merged both paths into vmcnt(0) waits in
-          // the last k-step, i.e. waited for these loads there
-          load_b(0, bnext, b0);
+        for (int ks = 0; ks < PKS; ks += 2) {
+          load_b(ks + 1, bvoff, b1);
+          if constexpr (A2) load_afrag(ks + 1, a1, p4c);
+          else load_afrag(ks, a0, p4c);
+          __builtin_amdgcn_sched_barrier(0);
+          kstep(a0, b0, p4c);
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks == 0) { NRMS_PX_STAMP(1) }   // item setup + first k-step (B(0) / A fragment waits)
+          if (ks + 2 < PKS) {
+            load_b(ks + 2, bvoff, b0);
+            if constexpr (A2) load_afrag(ks + 2, a0, p4c);
+          } else {
+            // unconditional (the last item reloads its own first k-step): behind a
+            // branch, the waitcnt pass merged both paths into vmcnt(0) waits in
+            // the last k-step, i.e. waited for these loads there
+            load_b(0, bnext, b0);
+          }
+          if constexpr (!A2) load_afrag(ks + 1, a0, p4c);
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (A2) {
+            if (ks + 2 < PKS) kstep(a1, b1, p4c);
+            else kstep_final(a1, b1, p4c);
+          } else {
+            if (ks + 2 < PKS) kstep(a0, b1, p4c);
+            else kstep_final(a0, b1, p4c);
+          }
+          __builtin_amdgcn_sched_barrier(0);
         }
-        if constexpr (!A2) load_afrag(ks + 1, a0);
-        __builtin_amdgcn_sched_barrier(0);
-        if constexpr (A2) {
-          if (ks + 2 < PKS) kstep(a1, b1);
-          else kstep_final(a1, b1);
-        } else {
-          if (ks + 2 < PKS) kstep(a0, b1);
-          else kstep_final(a0, b1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
       for (int j = 0; j < C; ++j) bvoff[j] = bnext[j];
@@ -655,9 +683,13 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
       }
     }
   };
-  if constexpr (NW == 4) run(std::integral_constant<int, PTW>{});
-  else if (w < 4) run(std::integral_constant<int, 3>{});
-  else run(std::integral_constant<int, 2>{});
+  auto run_w = [&](auto p4c) __attribute__((always_inline)) {
+    if constexpr (NW == 4) run(std::integral_constant<int, PTW>{}, p4c);
+    else if (w < 4) run(std::integral_constant<int, 3>{}, p4c);
+    else run(std::integral_constant<int, 2>{}, p4c);
+  };
+  if (!H3 || p4) run_w(std::true_type{});
+  else run_w(std::false_type{});
 #ifdef NRMS_PX_TIMING
   if (lane == 0) {
     unsigned long long* dbg = reinterpret_cast<unsigned long long*>(const_cast<float*>(packed) + OFF_STAMP);
@@ -697,6 +729,16 @@ int32_t launch_forward_pack(const WeightRows& wn, float* pn, const WeightRows& w
 }
 
 namespace {
+// NRMS_PROJ_PRODUCTS=4: the split-f16 projection on four products for every
+// column (A/B and the bitwise comparisons of tests/test_gpu_parity.py)
+int proj_force4() {
+  static const int v = [] {
+    const char* e = env_knob("NRMS_PROJ_PRODUCTS");
+    return (e && e[0] == '4') ? 1 : 0;
+  }();
+  return v;
+}
+
 template <bool SCATTER, bool H3>
 void launch_proj_kernel(int64_t grid, const float* X, int64_t n_rows_x, ARows ar, const int64_t* row_ids, int64_t M,
                         const float* packed, float* Y, int64_t ldy, const int32_t* m_dev, const tl::TailJobs& tj,
@@ -707,7 +749,7 @@ void launch_proj_kernel(int64_t grid, const float* X, int64_t n_rows_x, ARows ar
   constexpr int NW = NRMS_PX_WAVES;
   ensure_dynamic_lds(reinterpret_cast<const void*>(&proj_qkv_kernel<SCATTER, NW, H3>), (int)P_LDS);
   hipLaunchKernelGGL((proj_qkv_kernel<SCATTER, NW, H3>), dim3((unsigned)grid), dim3(64 * NW), P_LDS, s, X, n_rows_x,
-                     ar, row_ids, M, packed, Y, ldy, m_dev, tj);
+                     ar, row_ids, M, packed, Y, ldy, m_dev, tj, proj_force4());
 }
 }  // namespace
 

@@ -510,6 +510,54 @@ def test_qkv_project_f16x3_range(device, M):
     assert np.isnan(g[inf_rows]).all()
 
 
+def test_qkv_project_product_count(tmp_path):
+    """The split-f16 projection runs three products (w_lo·a_hi, w_hi·a_lo,
+    w_hi·2^11 a_hi) unless some W column fits in 11 bits, where the fourth
+    (w_hi·r, A's bits past 22) makes it exact (proj_x6.hip header). Two child
+    processes, the default and NRMS_PROJ_PRODUCTS=4 (tests/proj_products_worker.py):
+    random weights -> the two differ (the default took three products) and
+    both are within 2e-6 of the fp64 oracle per row, the four-product rows no
+    further off than 1.5x the three-product rows' worst; an identity W_Q ->
+    the default took four products (bitwise equal to the forced run) and
+    Q = X exactly (elements past 2^-15 of their row's largest); the bench
+    slice's logits agree within 1e-6."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    outs = {}
+    for tag, env_add in (("default", {}), ("four", {"NRMS_PROJ_PRODUCTS": "4"})):
+        env = dict(os.environ, **env_add)
+        p = subprocess.run([sys.executable, os.path.join(root, "tests", "proj_products_worker.py"),
+                            str(tmp_path / f"{tag}.npz")], env=env, capture_output=True, text=True, timeout=300)
+        assert p.returncode == 0, p.stderr[-3000:]
+        outs[tag] = np.load(tmp_path / f"{tag}.npz")
+    d, f = outs["default"], outs["four"]
+    X = d["X"].astype(np.float64)
+    sd = W.nrms_state(5, 64)
+    p_ = "news_encoder.multihead_self_attention"
+    want = np.concatenate([O.linear(X, sd[f"{p_}.{n_}.weight"], sd[f"{p_}.{n_}.bias"], np.float64)
+                           for n_ in ("W_Q", "W_K", "W_V")], axis=1)
+    assert not np.array_equal(d["rand"].view(np.uint32), f["rand"].view(np.uint32))
+    e3 = O.normwise_rel_err(d["rand"], want)
+    e4 = O.normwise_rel_err(f["rand"], want)
+    print(f"three products: worst {e3.max():.3e} mean {e3.mean():.3e}; four: worst {e4.max():.3e} mean {e4.mean():.3e}")
+    assert e3.max() < 2e-6 and e4.max() < 2e-6
+    assert e4.max() <= 1.5 * e3.max()
+    assert np.array_equal(d["mixed"].view(np.uint32), f["mixed"].view(np.uint32))
+    # Q = X bit for bit where the element's pieces are fp16 normals or exact
+    # subnormals (|x| >= 2^-15 of its row's largest); the smaller ones within
+    # 2^-30 of it
+    q, x = d["mixed"][:, :300], d["X"]
+    rmax = np.abs(x).max(axis=1, keepdims=True)
+    big = np.abs(x) >= rmax * 2.0 ** -15
+    assert big.mean() > 0.999
+    assert np.array_equal(q[big].view(np.uint32), x[big].view(np.uint32))
+    assert (np.abs(q - x) <= rmax * 2.0 ** -30).all()
+    rel = np.abs(d["logits"] - f["logits"]).max() / np.abs(f["logits"]).max()
+    assert rel < 1e-6, rel
+
+
 @pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("mode", [1, 2])
 def test_plan_matches_forward(device, fused, mode, gemm_mode):
