@@ -137,7 +137,7 @@ __device__ __forceinline__ void pack_proj(int idx, const WeightRows& w, float* _
 
 // H3: one wave per W row n < 16 PNT (rows past N: zeros), lane k = lane + 64 i
 // (i < 5 covers the K padding to 320): the row's max |w| (wave reduction)
-// gives its exponent ew; [ks][nt][plane hi | lo][lane][8 f16] as the x6
+// gives its exponent ew; [ks][nt][plane hi | 2^-11 lo][lane][8 f16] as the x6
 // fragments; lane 0 writes the bias, ew and whether the column can do
 // without the projection's fourth product (an element of the row has bits
 // past hi, so lo != 0; columns past N: yes). Block
@@ -169,8 +169,10 @@ __device__ __forceinline__ void pack_proj_h3(int b, int t, const WeightRows& w, 
     const int k = lane + 64 * i, ks = k >> 5, kq = (k >> 3) & 3;
     const float x = ldexpf(v[i], -ew);
     const _Float16 hi = (_Float16)x;
-    const float r1 = (x - (float)hi) * kTwo11;   // exact
-    const _Float16 lo = (_Float16)r1;
+    // lo plane at 2^-11 of the split's: it multiplies the staged 2^11 a_hi
+    // (a fp16 subnormal below 2^-14: bits lost only where the element is
+    // under 2^-18 of its column's largest)
+    const _Float16 lo = (_Float16)(x - (float)hi);
     inexact |= !(x == (float)hi);                 // bits past 11 (NaN: inexact)
     const int e = ((ks * PNT + nt) * 2) * 512 + (r + 16 * kq) * 8 + (k & 7);
     o[e] = hi;
@@ -239,8 +241,8 @@ __global__ __launch_bounds__(256) void forward_pack_kernel(WeightRows wn, float*
 // NW waves: 4 (one per SIMD, five N tiles each) or 8 (two per SIMD: waves
 // w < 4 three tiles, w >= 4 two, so each SIMD still owns five tiles of an
 // item and one wave's waits / stores run under its partner's MFMAs).
-// H3: the split-f16 arithmetic above (A planes hi | lo | r in LDS, W planes
-// hi | lo), else x6.
+// H3: the split-f16 arithmetic above (A planes 2^11 hi | lo | r in LDS, W
+// planes hi | 2^-11 lo), else x6.
 template <bool SCATTER, int NW, bool H3>
 __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __restrict__ X, int64_t n_rows_x, ARows ar,
                                                             const int64_t* __restrict__ row_ids, int64_t M,
@@ -379,7 +381,8 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
           }
           _Float16* d = reinterpret_cast<_Float16*>(As) + ar_ * PRB + 4 * c4;
           typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-          *reinterpret_cast<f16x4*>(d) = f16x4{h[0], h[1], h[2], h[3]};
+          // plane 0 holds 2^11 hi (exact: |hi| <= 16)
+          *reinterpret_cast<f16x4*>(d) = f16x4{h[0], h[1], h[2], h[3]} * (_Float16)kTwo11;
           *reinterpret_cast<f16x4*>(d + PKP) = f16x4{l[0], l[1], l[2], l[3]};
           if (p4) *reinterpret_cast<f16x4*>(d + 2 * PKP) = f16x4{r[0], r[1], r[2], r[3]};
         }
@@ -462,7 +465,7 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
       }
     };
     // A fragments of one k-step in the order the products use them (x6: lo
-    // planes first; H3: hi, lo, hi')
+    // planes first; H3: 2^11 hi, lo, r)
     auto load_afrag = [&](int ks, frag (&a)[PMT][3], auto p4c) __attribute__((always_inline)) {
       constexpr int NAP = (H3 && !decltype(p4c)::value) ? 2 : 3;   // A planes read
 #pragma unroll
@@ -482,31 +485,25 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
       else
         acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bb[j][PB], a[mt][PA], acc[mt][j], 0, 0, 0);
     };
-    // H3: 2^11 a = 2^11 hi + lo + r exactly; with w = hi + 2^-11 lo the four
-    // products w_hi·r, w_lo·a_hi, w_hi·a_lo, w_hi·(2^11 a_hi) (formed in
-    // registers, exact) accumulate 2^11 w·a
+    // H3: 2^11 a = 2^11 hi + lo + r exactly; with w = hi + 2^-11 lo the
+    // products w_hi·r (P4), w_lo·a_hi, w_hi·a_lo, w_hi·(2^11 a_hi) accumulate
+    // 2^11 w·a. The A planes in LDS are [2^11 hi | lo | r] and the W lo plane
+    // is packed at 2^-11, so w_lo·a_hi = (2^-11 w_lo)·(2^11 hi): every product
+    // is one plane pair, no operand formed in registers.
     auto mfma_h = [&](const frag& b, const frag& a, int mt, int j) __attribute__((always_inline)) {
       acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc[mt][j], 0, 0, 0);
     };
-    auto hi_scaled = [&](const frag (&a)[PMT][3], frag (&hs)[PMT]) __attribute__((always_inline)) {
-#pragma unroll
-      for (int mt = 0; mt < PMT; ++mt) hs[mt] = a[mt][0] * (_Float16)kTwo11;
-    };
+    // product p: (W plane, A plane) = (hi, r), (lo, 2^11 hi), (hi, lo), (hi, 2^11 hi)
+    auto pw = [](int p) constexpr { return p == 1 ? 1 : 0; };
+    auto pa = [](int p) constexpr { return p == 0 ? 2 : p == 2 ? 1 : 0; };
     auto kstep = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL], auto p4c) __attribute__((always_inline)) {
       if constexpr (H3) {
 #pragma unroll
-        for (int p = decltype(p4c)::value ? 0 : 1; p < 3; ++p)
+        for (int p = decltype(p4c)::value ? 0 : 1; p < 4; ++p)
 #pragma unroll
           for (int j = 0; j < C; ++j)
 #pragma unroll
-            for (int mt = 0; mt < PMT; ++mt)
-              mfma_h(bb[j][p == 1 ? 1 : 0], a[mt][p == 0 ? 2 : p == 1 ? 0 : 1], mt, j);
-        frag hs[PMT];
-        hi_scaled(a, hs);
-#pragma unroll
-        for (int j = 0; j < C; ++j)
-#pragma unroll
-          for (int mt = 0; mt < PMT; ++mt) mfma_h(bb[j][0], hs[mt], mt, j);
+            for (int mt = 0; mt < PMT; ++mt) mfma_h(bb[j][pw(p)], a[mt][pa(p)], mt, j);
       } else {
         constexpr int pa_[6] = {2, 1, 0, 1, 0, 0}, pb_[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
@@ -607,8 +604,6 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
       // the kernel; here they run under the MFMAs)
       auto kstep_final = [&](const frag (&a)[PMT][3], const frag (&bb)[C][NPL], auto p4c)
           __attribute__((always_inline)) {
-        [[maybe_unused]] frag hs[PMT];
-        if constexpr (H3) hi_scaled(a, hs);
 #pragma unroll
         for (int j = 0; j < C; ++j) {
           if constexpr (H3) {
@@ -616,7 +611,7 @@ __global__ __launch_bounds__(64 * NW, 1) void proj_qkv_kernel(const float* __res
             for (int p = decltype(p4c)::value ? 0 : 1; p < 4; ++p)
 #pragma unroll
               for (int mt = 0; mt < PMT; ++mt)
-                mfma_h(bb[j][p == 1 ? 1 : 0], p == 3 ? hs[mt] : a[mt][p == 0 ? 2 : p == 1 ? 0 : 1], mt, j);
+                mfma_h(bb[j][pw(p)], a[mt][pa(p)], mt, j);
           } else {
             constexpr int pa_[6] = {2, 1, 0, 1, 0, 0}, pb_[6] = {0, 1, 2, 0, 1, 0};
 #pragma unroll
