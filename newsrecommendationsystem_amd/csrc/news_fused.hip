@@ -139,7 +139,7 @@ __global__ __launch_bounds__(256) void pack_additive_b_kernel(const float* __res
                                                               float* __restrict__ WaP,
                                                               int32_t* __restrict__ recheck_count) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx < pk::NEWS_NCOUNT)   // [recheck count, bucket counts x5, rep, user row-list count]
+  if (idx < pk::NEWS_NCOUNT)   // [recheck count, bucket counts x5, rep, user row-list count, group claims, spare]
     recheck_count[idx] = idx == pk::NEWS_CNT_REP ? INT32_MAX : 0;
   if (idx >= WAP_FLOATS + SPECIAL_FLOATS) return;
   if (idx >= WAP_FLOATS) {
@@ -202,8 +202,8 @@ static_assert(pk::NEWS_COUNTERS == WAP_MAX + SPECIAL_FLOATS + WAP2_FLOATS, "pack
 // Without compaction every title is one 20-row slot (NB = 5).
 constexpr int NBK = tl::NBK;                             // buckets NB = 1..5
 constexpr int NCNT = pk::NEWS_NCOUNT;                    // int32 counters of a launch
-constexpr int CNT_RECHECK = 0, CNT_BUCKET = tl::CNT_BUCKET, CNT_REP = pk::NEWS_CNT_REP, CNT_USER = 7;
-static_assert(CNT_BUCKET + NBK == CNT_REP && CNT_USER < NCNT && tl::FL == FL, "counter layout");
+constexpr int CNT_RECHECK = 0, CNT_BUCKET = tl::CNT_BUCKET, CNT_REP = pk::NEWS_CNT_REP, CNT_USER = 7, CNT_CLAIM = 8;
+static_assert(CNT_BUCKET + NBK == CNT_REP && CNT_CLAIM < NCNT && NCNT % 4 == 0 && tl::FL == FL, "counter layout");
 
 using tl::RowMap;   // q|k|v row of token i of title s
 using tl::Titles;   // the classification's output
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   float* part = X6 ? lds + FROWS * XRB / 2 : (H3 ? lds + FROWS * XRH / 2 : ctxL + FROWS * SC);   // [80][8] row partials
   const float** rowptr = reinterpret_cast<const float**>(part + PART_STRIDE * FROWS);   // [RPB][4 titles][20 slots]
   int32_t* tmeta = reinterpret_cast<int32_t*>(rowptr + RPB * FROWS);   // [RPB][title index x4 | count x4]
-  int32_t* sched = tmeta + 8 * RPB;   // [gend x NBK | bucket counts x NBK | rep | groups] (see below)
+  int32_t* sched = tmeta + 8 * RPB;   // [gend x NBK | bucket counts x NBK | rep | groups | claim] (see below)
 
   const int tid = threadIdx.x, lane = tid & 63, w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const float* zero_row = WaP + WAP_MAX;
@@ -715,6 +715,11 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
 #endif
 
   int it = 0;
+  // main pass: the launch's group-claim counter (reset by the pack kernel)
+  // and the last claim, read back by every wave
+  const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<int32_t*>(ts.counters + CNT_CLAIM), 0, 4, 0x00020000);
+  int32_t q_claim = 0;
   // H3: the first k-step's W_add fragments are loaded at the end of phase A,
   // before the A -> B barrier: the barrier wait covers their L2 latency
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(
@@ -724,22 +729,29 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
   for (int j = 0; j < 4; ++j) wvoff[j] = lane * 16 + (j < 3 ? 3 * w + j : 12) * 3 * 1024;
   f16x8 wb0[4][3];
   // one iteration: group key_at(idx), of bucket NB - 1
-  auto iterate = [&](int32_t idx, auto nbc) {
+  // iterate(idx, idx_n, idx_n3): this group, the next, and the one three
+  // ahead (its title indices are read at this group's end)
+  auto iterate = [&](int32_t idx, int32_t idx_n, int32_t idx_n3, auto nbc) {
     constexpr int NB = decltype(nbc)::value;
     int tmask, tmask_n;
     const int32_t k = key_at(idx, tmask);
     int32_t g, gn = 0;
     bucket_of(k, g);
-    const int32_t kn = key_at(idx + (int32_t)gridDim.x, tmask_n);
-    const int bn = (idx + (int32_t)gridDim.x < n_iter) ? bucket_of(kn, gn) : -1;
+    const int32_t kn = key_at(idx_n, tmask_n);
+    const int bn = (idx_n < n_iter) ? bucket_of(kn, gn) : -1;
     const int nb_next = bn + 1;   // 0: no next group
     // the group after next has its row pointers staged during this attention
     // (its title indices were read at the end of the previous group: s_carry);
     // the group after that has its title indices read at the end of this one
     int tmask_n3;
     int32_t gn3 = 0;
-    const int32_t kn3 = key_at(idx + 3 * (int32_t)gridDim.x, tmask_n3);
-    const int bn3 = (idx + 3 * (int32_t)gridDim.x < n_iter) ? bucket_of(kn3, gn3) : -1;
+    const int32_t kn3 = key_at(idx_n3, tmask_n3);
+    const int bn3 = (idx_n3 < n_iter) ? bucket_of(kn3, gn3) : -1;
+    // main pass: claim the group four ahead (wave 0 lane 0's offset is the
+    // only one in range: no branch around the atomic, whose return the
+    // waitcnt pass would otherwise wait for at the branch's join)
+    [[maybe_unused]] int32_t claim_v = 0;
+    if constexpr (!EXACT) claim_v = __builtin_amdgcn_raw_ptr_buffer_atomic_add_i32(1, crs, tid == 0 ? 0 : 64, 0, 0);
     // row-pointer buffers: this group's, the next group's, the one after's
     const int buf = it & (RPB - 1), nbuf = (it + 1) & (RPB - 1), nbuf2 = (it + 2) & (RPB - 1);
     {
@@ -1141,6 +1153,8 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
         }
       }
       NRMS_STAMP(4)
+      if constexpr (!EXACT)
+        if (tid == 0) sched[2 * NBK + 2] = claim_v;   // (read after the barrier; rewritten after the next A -> B barrier)
       __syncthreads();   // row partials complete
       NRMS_STAMP(5)
 
@@ -1244,6 +1258,7 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
       }
       NRMS_STAMP(6)
     }
+    if constexpr (!EXACT) q_claim = __builtin_amdgcn_readfirstlane(sched[2 * NBK + 2]);
     ++it;
   };
   if constexpr (EXACT) {
@@ -1251,25 +1266,37 @@ __global__ __launch_bounds__(NTHR, 1) void fused_news_kernel(
     for (int32_t idx = blockIdx.x; idx < n_iter; idx += gridDim.x) {
       int tm;
       int32_t g;
+      const int32_t i1 = idx + (int32_t)gridDim.x, i3 = idx + 3 * (int32_t)gridDim.x;
       switch (bucket_of(key_at(idx, tm), g)) {
-        case 0: iterate(idx, std::integral_constant<int, 1>{}); break;
-        case 1: iterate(idx, std::integral_constant<int, 2>{}); break;
-        case 2: iterate(idx, std::integral_constant<int, 3>{}); break;
-        case 3: iterate(idx, std::integral_constant<int, 4>{}); break;
-        default: iterate(idx, std::integral_constant<int, 5>{}); break;
+        case 0: iterate(idx, i1, i3, std::integral_constant<int, 1>{}); break;
+        case 1: iterate(idx, i1, i3, std::integral_constant<int, 2>{}); break;
+        case 2: iterate(idx, i1, i3, std::integral_constant<int, 3>{}); break;
+        case 3: iterate(idx, i1, i3, std::integral_constant<int, 4>{}); break;
+        default: iterate(idx, i1, i3, std::integral_constant<int, 5>{}); break;
       }
     }
   } else {
-    // the main pass walks the buckets' contiguous group ranges one after the
-    // other, one loop per NB (a single loop switching between the five bodies
-    // spilled ~600 registers)
+    // The main pass walks the groups in order (buckets NB = 5 .. 1, one loop
+    // per NB: a single loop switching between the five bodies spilled ~600
+    // registers). A workgroup's first four groups are blockIdx.x + p grid
+    // (p < 4, the prologue's); each iteration then claims the group four
+    // ahead from a launch counter (4 grid + claims so far), so the
+    // workgroups that drew lighter groups take more of them: with the static
+    // stride the slowest workgroup ran 1.9 % past the mean
+    // (profiles/r6/r6s_news_balance.txt). Claims are increasing per workgroup,
+    // so the next group is of this bucket or a smaller one, as before.
+    const int32_t grid = gridDim.x;
+    int32_t q0 = (int32_t)blockIdx.x, q1 = q0 + grid, q2 = q1 + grid, q3 = q2 + grid;
     auto run_bucket = [&](auto nbc) {
       constexpr int NB = decltype(nbc)::value;
-      const int32_t start = NB == NBK ? 0 : __builtin_amdgcn_readfirstlane(sched[NB]);
       const int32_t end = __builtin_amdgcn_readfirstlane(sched[NB - 1]);
-      const int32_t grid = gridDim.x;
-      int32_t idx = start + (((int32_t)blockIdx.x - start) % grid + grid) % grid;
-      for (; idx < end; idx += grid) iterate(idx, nbc);
+      while (q0 < end) {
+        iterate(q0, q1, q3, nbc);
+        q0 = q1;
+        q1 = q2;
+        q2 = q3;
+        q3 = 4 * grid + q_claim;
+      }
     };
     run_bucket(std::integral_constant<int, 5>{});
     run_bucket(std::integral_constant<int, 4>{});

@@ -23,7 +23,7 @@ constexpr int NEWS_SPECIAL = 2 * ROW;
 constexpr int NEWS_COUNTERS = NEWS_WAP_MAX + NEWS_SPECIAL + NEWS_WAP_X6;   // int32 [NEWS_NCOUNT] after the f16 planes
 // the news launch's counters: [recheck count, title-bucket counts 0..4, rep
 // title (INT32_MAX: none), user row-list count]
-constexpr int NEWS_NCOUNT = 8, NEWS_CNT_REP = 6;
+constexpr int NEWS_NCOUNT = 12, NEWS_CNT_REP = 6;   // (a multiple of 4: the arrays after them stay 16-B aligned)
 constexpr int NEWS_X6_ELEMS = KS * NT * 64 * 8;   // threads of the x6 / f16 packing
 constexpr int USER_X6_ELEMS = KS * NT * 64 * 8;
 constexpr int USER_F32_ELEMS = KG * NT * 64 * 4;

@@ -11,6 +11,7 @@
 #endif
 #include "../../newsrecommendationsystem_amd/csrc/news_fused.hip"
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -119,6 +120,19 @@ int main(int argc, char** argv) {
         printf(" %s=%.0f", names[k], s);
       }
       printf(" | total=%.0f\n", tot);
+    }
+    {
+      // per-workgroup busy cycles (wave 0, all phases): the persistent grid's
+      // balance -- max over mean is the tail the static group stride leaves
+      std::vector<double> tb(256, 0.0);
+      for (int blk = 0; blk < 256; ++blk)
+        for (int k = 0; k < nk; ++k) tb[blk] += (double)h_dbg[(blk * nwaves[var]) * 8 + k];
+      std::vector<double> srt = tb;
+      std::sort(srt.begin(), srt.end());
+      double mean = 0;
+      for (double v : tb) mean += v / 256;
+      printf("  workgroup totals: min %.0f p10 %.0f median %.0f p90 %.0f max %.0f mean %.0f (max/mean %.4f)\n",
+             srt[0], srt[25], srt[128], srt[230], srt[255], mean, srt[255] / mean);
     }
 #endif
   }
