@@ -107,9 +107,10 @@ typedef enum { NRMS_PROJ_AUTO = 0, NRMS_PROJ_DIRECT = 1, NRMS_PROJ_FOLDED = 2 } 
  * projections (nrms_qkv_project_ws, nrms_forward, the encode entry points)
  * scale every input row and every weight row by a power of two into fp16's
  * range (exact, any magnitude), split the input exactly into three fp16
- * pieces and the weights into two (22 bits), and accumulate four products:
- * fp32-GEMM accuracy, and products as exact as fp32's for weights that fit
- * in 11 bits. The fused UserEncoder's additive GEMM scales each context row
+ * pieces and the weights into two (22 bits), and accumulate three products
+ * (four when some weight column fits in 11 bits; NRMS_PROJ_PRODUCTS=4 forces
+ * four): fp32-GEMM accuracy, and products as exact as fp32's for weights
+ * that fit in 11 bits. The fused UserEncoder's additive GEMM scales each context row
  * the same way and accumulates three fp16 products (22-bit operands). The
  * staged nrms_qkv_project and the stage kernels run SPLIT_BF16X6 in this mode.
  * F32: v_mfma_f32_16x16x4_f32, each product an exact fp32 FMA.
@@ -194,9 +195,10 @@ int32_t nrms_qkv_project(const float* x, int64_t n_rows_x, const int64_t* row_id
  * NRMS_GEMM_F32 (both run the f32 GEMM). Under NRMS_GEMM_SPLIT_F16X3 (the
  * default) it runs the scaled split-f16 arithmetic instead — each x row and
  * each weight row scaled by a power of two into fp16's range, x split exactly
- * into three fp16 pieces, the weight into two (22 bits), four products summed
- * in fp32: within ~2^-22 |x||w| per product of the exact result (fp32-GEMM
- * accuracy; exact products for weights that fit in 11 bits) — so only within
+ * into three fp16 pieces, the weight into two (22 bits), three products
+ * summed in fp32 (four when some weight column fits in 11 bits): within
+ * ~2^-22 |x||w| per product of the exact result (fp32-GEMM accuracy; exact
+ * products for weights that fit in 11 bits) — so only within
  * rounding of nrms_qkv_project's x6 rows, not bitwise. Other shapes: as
  * nrms_qkv_project. */
 size_t nrms_qkv_project_workspace_size(int32_t D);
