@@ -58,7 +58,10 @@ constexpr int PK = 300, PN = 900;
 constexpr int PKS = 10;                          // k-steps of 32 (K padded to 320)
 constexpr int PKP = PKS * 32;                    // 320
 constexpr int PNT = (PN + 15) / 16;              // 57 N tiles (the last: 4 live columns)
-constexpr int PM = 64;                           // A rows per tile
+#ifndef NRMS_PX_PM   // (probe: other tile heights; profiles/r6/r6w_proj_tile_height_ab.txt)
+#define NRMS_PX_PM 64
+#endif
+constexpr int PM = NRMS_PX_PM;                   // A rows per tile
 constexpr int PMT = PM / 16;                     // 4 M tiles
 constexpr int PTW = 5;                           // N tiles per wave per item
 constexpr int PRANGE = 4 * PTW;                  // N tiles per item

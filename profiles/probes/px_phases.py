@@ -39,3 +39,14 @@ print("%d waves; total cycles per wave: mean %.0f max %.0f" % (nw, tot.mean(), t
 for k, n in enumerate(names[:7]):
     v = stamps[:, :, k]
     print(f"{n:20s} mean {v.mean():10.0f}  max {v.max():10.0f}")
+# per-workgroup busy cycles (max over its waves): the static item ranges' balance
+wg = tot.max(axis=1)
+print("workgroup totals: min %.0f p10 %.0f median %.0f p90 %.0f max %.0f mean %.0f (max/mean %.4f)"
+      % (wg.min(), np.percentile(wg, 10), np.median(wg), np.percentile(wg, 90), wg.max(), wg.mean(), wg.max() / wg.mean()))
+# by XCD (workgroups b, b + 8, .. share one: MI355X_MICROARCH.md dispatch notes)
+# and by position in the grid
+for x in range(8):
+    v = wg[x::8]
+    print("xcd-slot %d: mean %.0f max %.0f" % (x, v.mean(), v.max()))
+q = len(wg) // 4
+print("grid quarters (mean):", " ".join("%.0f" % wg[i * q:(i + 1) * q].mean() for i in range(4)))
