@@ -50,3 +50,8 @@ for x in range(8):
     print("xcd-slot %d: mean %.0f max %.0f" % (x, v.mean(), v.max()))
 q = len(wg) // 4
 print("grid quarters (mean):", " ".join("%.0f" % wg[i * q:(i + 1) * q].mean() for i in range(4)))
+# per wave class: waves 0-3 hold three N tiles per item, waves 4-7 two
+if nw == 8:
+    for lo, hi, tag in ((0, 4, "waves 0-3 (3 tiles)"), (4, 8, "waves 4-7 (2 tiles)")):
+        v = stamps[:, lo:hi]
+        print(tag + ": " + " ".join("%s=%.0f" % (names[k], v[:, :, k].mean()) for k in range(7)))
