@@ -631,6 +631,35 @@ def test_split_gemm_accuracy_matches_f32(device):
         assert e[0] <= 2 * f32[0] + 1e-7 and e[1] <= 2 * f32[1] + 1e-7, errs
 
 
+def test_forward_bitwise_under_scheduling_perturbation(device):
+    """The news kernel claims its groups at run time (round 6) and the
+    projections / UserEncoder are persistent or LPT-ordered: which workgroup
+    computes a title or a user changes from run to run. The bench batch's
+    logits (1,024 impressions) are bitwise the same across repeated
+    nrms_forward calls, alone and with a second stream keeping CUs busy with
+    GEMMs while they run (a different workgroup timing, hence different
+    claims)."""
+    import bench
+    from newsrecommendationsystem_amd import stream as S
+    model = bench.build_model(device)
+    idx = bench.stream_impressions(0, 1, 1024, device)
+    cand, clk = S.batch(0, idx, bench.V_WORDS)
+    with torch.no_grad():
+        ref = model.forward_ids(cand, clk).clone()
+        assert torch.isfinite(ref).all()
+        side = torch.cuda.Stream(device)
+        a = torch.randn(4096, 4096, device=device)
+        for rep in range(6):
+            if rep % 2:
+                side.wait_stream(torch.cuda.current_stream(device))
+                with torch.cuda.stream(side):
+                    for _ in range(4):
+                        a = torch.tanh(a @ a * 1e-3)
+            y = model.forward_ids(cand, clk)
+            torch.cuda.synchronize()
+            assert torch.equal(y.view(torch.int32), ref.view(torch.int32)), rep
+
+
 def test_bench_batch_slice_gemm_arith_vs_fp64(device):
     """A 128-impression slice of the bench's own config-3 batch (bench.py's
     model: N(0,1) embedding, V = 70,976; the first 128 impressions of the
