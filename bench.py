@@ -442,7 +442,19 @@ def launch_ranks(n, backend):
            "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
            os.path.abspath(__file__), *sys.argv[1:]]
     env = dict(os.environ, NRMS_BENCH_LAUNCHER="bench.py --gpus (torch.distributed.run child)")
-    return subprocess.call(cmd, env=env)
+    # relay rank 0's JSON line alone to stdout; anything else the ranks print
+    # there (gloo's connection notices, from its C++ side) goes to stderr
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in p.stdout:
+        at = line.find('{"metric"')
+        if at >= 0:
+            sys.stdout.write(line[at:])
+            sys.stdout.flush()
+            if at > 0:
+                sys.stderr.write(line[:at] + "\n")
+        else:
+            sys.stderr.write(line)
+    return p.wait()
 
 
 def fedavg_sync_leg(model, device, dist, reps=5):

@@ -271,6 +271,8 @@ def test_bench_gpus2_self_launch_gloo(tmp_path):
                          env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
     rec = _check_weak_record(two, 2, "gloo")
     assert rec["world_size"] == 2 and "child" in rec["launcher"]
+    # stdout holds the JSON line and nothing else (gloo's notices go to stderr)
+    assert len(two.stdout.strip().splitlines()) == 1, two.stdout[-2000:]
     fa = rec["fedavg_sync"]
     assert fa["world"] == 2 and fa["params"] == 21955400 and fa["fedavg_sync_ms"] > 0
     for r in range(2):
