@@ -526,8 +526,9 @@ def test_qkv_project_product_count(tmp_path):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     outs = {}
+    base = {k: v for k, v in os.environ.items() if k != "NRMS_PROJ_PRODUCTS"}
     for tag, env_add in (("default", {}), ("four", {"NRMS_PROJ_PRODUCTS": "4"})):
-        env = dict(os.environ, **env_add)
+        env = dict(base, **env_add)
         p = subprocess.run([sys.executable, os.path.join(root, "tests", "proj_products_worker.py"),
                             str(tmp_path / f"{tag}.npz")], env=env, capture_output=True, text=True, timeout=300)
         assert p.returncode == 0, p.stderr[-3000:]
