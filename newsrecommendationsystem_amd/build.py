@@ -30,6 +30,10 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, 
 # the hot phases, so the news kernel took the default; after the round-4
 # pipeline changes max-ILP is 0.9 % faster end to end (news_fused -3.7 us,
 # 44 B of scratch per lane against 8; profiles/r4r2_news_sched_ab.txt).
+# Round 6 re-check (profiles/r6/r7k_sched_strategy_ab.txt, r7l_user_maxilp_ab.txt,
+# same box x3 each): news_fused under the default scheduler and proj_x6 under
+# max-ILP within noise; the UserEncoder under max-ILP user_fused -0.7..-1.4 %
+# but the graph-replayed step +0.25 % / -0.2 % -- not taken.
 FILE_FLAGS = {
     "gemm_f32.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
     "news_fused.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
